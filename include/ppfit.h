@@ -1,0 +1,178 @@
+/*
+ * ppfit.h -- C ABI of libppfit.so, the MI355X (gfx950) implementation of the
+ * PulsePortraiture wideband FFTFIT hot path.
+ *
+ * The reference (kmjc/PulsePortraiture) is pure Python; its "plugin surface"
+ * is the set of Python call signatures listed in SURVEY.md §8(b).  Each entry
+ * point below is what the Python drop-ins in pulseportraiture_amd/ bind via
+ * ctypes in place of the reference's numpy/scipy code:
+ *
+ *   ppf_fit_portrait_batch  <- pptoaslib.fit_portrait_full   pptoaslib.py:928-1096
+ *                              (+ the get_TOAs initial guess pptoas.py:420-456,
+ *                               ppalign.py:180-185, batched over subints)
+ *   ppf_phase_shift_batch   <- pplib.fit_phase_shift          pplib.py:2054-2100
+ *   ppf_rotate_rows         <- pplib.rotate_data / rotate_portrait /
+ *                              pptoaslib.rotate_portrait_full pplib.py:2338-2460,
+ *                                                             pptoaslib.py:52-81
+ *   ppf_rotate_accumulate   <- ppalign.align_archives' weighted sum
+ *                              ppalign.py:202-208
+ *   ppf_irfft_rows          <- numpy.fft.irfft (final step of ppalign.py:210-213)
+ *   ppf_noise_rows          <- pplib.get_noise_PS(chans=True)  pplib.py:2227-2253
+ *   ppf_synth_portraits     <- (test/bench input producer; pplib.make_fake_pulsar
+ *                              math, pplib.py:3342-3377, on device)
+ *
+ * Conventions
+ *  - Every array argument is a DEVICE pointer (hipMalloc'd or a torch CUDA
+ *    tensor's data_ptr) unless documented otherwise; arrays are C-order fp64.
+ *  - Calls are stream-ordered on the context's stream (ppf_set_stream); they
+ *    do not synchronise unless stated.  One context per device per host
+ *    thread; a context is not re-entrant.
+ *  - Return codes: PPF_OK (0) or a negative PPF_ERR_*; ppf_last_error()
+ *    describes the last failure.  Per-subint solver status follows scipy's
+ *    trust-ncg codes (0 gradient small / NaN, 1 maxiter, 2 no predicted
+ *    reduction, 3 linalg error), as returned by the reference's
+ *    results.status (pptoaslib.py:1018).
+ *  - nbin must be a power of two in [16, 8192]; nchan <= PPF_MAX_NCHAN.
+ */
+#ifndef PPFIT_H
+#define PPFIT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PPF_OK 0
+#define PPF_ERR_INVALID -1
+#define PPF_ERR_DEVICE -2
+#define PPF_ERR_UNSUPPORTED -3
+#define PPF_ERR_NOMEM -4
+
+#define PPF_MAX_NCHAN 2048
+#define PPF_VERSION 1
+
+/* kernel ids for ppf_get_kernel_time */
+#define PPF_K_MODEL_FFT 0
+#define PPF_K_DATA_XSPEC 1
+#define PPF_K_FIT 2
+#define PPF_K_PHASE_SHIFT 3
+#define PPF_K_ROTATE 4
+#define PPF_K_ROT_ACCUM 5
+#define PPF_K_SYNTH 6
+#define PPF_K_IRFFT 7
+#define PPF_K_NOISE 8
+#define PPF_NUM_KERNELS 9
+
+typedef struct ppf_ctx ppf_ctx;
+
+int ppf_version(void);
+int ppf_ctx_create(int device, ppf_ctx** out);
+void ppf_ctx_destroy(ppf_ctx* ctx);
+const char* ppf_last_error(const ppf_ctx* ctx);
+/* hip stream (hipStream_t cast to void*); NULL selects the null stream */
+int ppf_set_stream(ppf_ctx* ctx, void* stream);
+int ppf_synchronize(ppf_ctx* ctx);
+/* Upper bound on workspace bytes the context may hold (default 32 GiB). */
+int ppf_set_workspace_limit(ppf_ctx* ctx, int64_t bytes);
+/* Per-kernel HIP-event timing on the context stream (off by default). */
+int ppf_set_timing(ppf_ctx* ctx, int enable);
+int ppf_get_kernel_time(ppf_ctx* ctx, int kernel_id, double* total_ms,
+                        int64_t* launches);
+int ppf_reset_kernel_times(ppf_ctx* ctx);
+
+/* ---------------------------------------------------------------------- */
+/* Batched wideband fit: fit_portrait_full over nsub subints.              */
+/* ---------------------------------------------------------------------- */
+#define PPF_METHOD_TRUST_NCG 0
+
+typedef struct {
+  int32_t nsub, nchan, nbin, nmodel;
+  int32_t fit_flags[5];   /* phi, DM, GM, tau, alpha (pptoaslib.py:928)     */
+  int32_t log10_tau;      /* fit log10(tau) instead of tau                 */
+  int32_t option;         /* get_nu_zeros option (pptoaslib.py:733)        */
+  int32_t method;         /* PPF_METHOD_TRUST_NCG                           */
+  int32_t is_toa;         /* pptoaslib.py:1048-1050                         */
+  int32_t guess;          /* 1: in-kernel initial phase guess (pptoas.py:420-456) */
+  int32_t guess_Ns;       /* opt.brute grid size (100 in pptoas, nbin in ppalign) */
+  int32_t guess_wrap;     /* 1: phase_transform(..., mod=True) to nu_fit_DM */
+  int32_t reserved;
+  const double* data;       /* [nsub][nchan][nbin]                          */
+  const double* model;      /* [nmodel][nchan][nbin]                        */
+  const int32_t* model_idx; /* [nsub] or NULL (all 0)                       */
+  const double* freqs;      /* [nsub][nchan] MHz                            */
+  const double* errs;       /* [nsub][nchan] time-domain sigma, or NULL:
+                               estimated as get_noise_PS (pplib.py:2227)    */
+  const uint8_t* chan_mask; /* [nsub][nchan] 1 = fit channel, or NULL       */
+  const double* weights;    /* [nsub][nchan] guess-average weights or NULL  */
+  const double* P;          /* [nsub] period, s                             */
+  const double* init;       /* [nsub][5] initial params                     */
+  const double* nu_fit;     /* [nsub][3] NaN -> mean of fitted freqs        */
+  const double* nu_out;     /* [nsub][3] NaN -> zero-covariance frequency   */
+  const double* guess_nu;   /* [nsub] dedispersion ref of the guess; NaN ->
+                               mean freq (pptoas) ; NULL -> NaN             */
+  const double* guess_tau;  /* [nsub] linear tau [rot] at nu_fit_tau applied
+                               to the guess template, or NULL (0)           */
+} ppf_fit_desc;
+
+typedef struct {
+  double* params;       /* [nsub][5] (phi at nu_DM, DM, GM, tau(log10?), alpha) */
+  double* param_errs;   /* [nsub][5]                                        */
+  double* nu_out;       /* [nsub][3] nu_DM, nu_GM, nu_tau                  */
+  double* cov;          /* [nsub][5][5] nfit x nfit block top-left           */
+  double* scales;       /* [nsub][nchan] (0 on masked channels)             */
+  double* scale_errs;   /* [nsub][nchan]                                    */
+  double* channel_snrs; /* [nsub][nchan]                                    */
+  double* chi2;         /* [nsub]                                           */
+  double* red_chi2;     /* [nsub]                                           */
+  double* snr;          /* [nsub]                                           */
+  int32_t* nfev;        /* [nsub]                                           */
+  int32_t* status;      /* [nsub]                                           */
+  double* init_used;    /* [nsub][5] or NULL: starting point after the guess */
+  double* fun;          /* [nsub] or NULL: final objective value            */
+  double* cov_nosc;     /* [nsub][5][5] or NULL: inv(0.5 H) of the curvature
+                           without amplitude terms at the output params
+                           (legacy pplib.fit_portrait errors, pplib.py:2184-2190) */
+} ppf_fit_result;
+
+int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* desc,
+                           const ppf_fit_result* out);
+
+/* ---------------------------------------------------------------------- */
+/* fit_phase_shift over nprof profiles (pplib.py:2054-2100).              */
+/* out[nprof][6] = phase, phase_err, scale, scale_err, snr, red_chi2       */
+/* noise: [nprof] time-domain sigma or NaN/NULL -> get_noise (PS)          */
+/* ---------------------------------------------------------------------- */
+int ppf_phase_shift_batch(ppf_ctx* ctx, int32_t nprof, int32_t nbin,
+                          const double* data, const double* model,
+                          const int32_t* model_idx, const double* noise,
+                          int32_t Ns, double lo, double hi, double* out);
+
+/* out[r] = irfft(rfft(in[r]) * exp(2 pi i k phase[r]))  (rotate_data)     */
+int ppf_rotate_rows(ppf_ctx* ctx, int32_t nrow, int32_t nbin, const double* in,
+                    const double* phase, double* out);
+
+/* accum[n][k] += sum_s weight[s][n] * rfft(data[s][n])[k] * e^{2 pi i k phase[s][n]}
+ * accum is complex [nchan][nbin/2+1] interleaved (re, im); weight 0 skips.  */
+int ppf_rotate_accumulate(ppf_ctx* ctx, int32_t nsub, int32_t nchan,
+                          int32_t nbin, const double* data, const double* phase,
+                          const double* weight, double* accum);
+
+/* out[r] = irfft(spec[r]) where spec is complex [nrow][nbin/2+1]           */
+int ppf_irfft_rows(ppf_ctx* ctx, int32_t nrow, int32_t nbin, const double* spec,
+                   double* out);
+
+/* out[r] = get_noise_PS(in[r]) (frac=4)                                   */
+int ppf_noise_rows(ppf_ctx* ctx, int32_t nrow, int32_t nbin, const double* in,
+                   double* out);
+
+/* data[s][n] = irfft(rfft(model[n]) * e^{2 pi i k phase[s][n]})
+ *              + sigma * N(0,1)[Philox4x32-10(seed; bin pair, n, s + sub0)] */
+int ppf_synth_portraits(ppf_ctx* ctx, int32_t nsub, int32_t nchan, int32_t nbin,
+                        const double* model, const double* phase, double sigma,
+                        uint64_t seed, int64_t sub0, double* data);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PPFIT_H */

@@ -1,0 +1,559 @@
+// ppfit_capi.hip -- host side of libppfit: context, workspace, launches.
+// Implements include/ppfit.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "ppfit.h"
+#include "ppfit_kernels.hpp"
+
+using namespace ppf;
+
+namespace {
+
+struct TimedLaunch {
+  int kid;
+  hipEvent_t a, b;
+};
+
+struct Buffer {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+}  // namespace
+
+struct ppf_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  int64_t ws_limit = (int64_t)32 << 30;
+  double2* tw[16] = {nullptr};
+  Buffer ws;      // per-chunk fit workspace
+  Buffer mspec;   // template spectra
+  Buffer aux;     // misc (synth templates, partial sums)
+  bool timing = false;
+  std::vector<TimedLaunch> pending;
+  std::vector<hipEvent_t> pool;
+  double ktime[PPF_NUM_KERNELS] = {0};
+  int64_t klaunch[PPF_NUM_KERNELS] = {0};
+};
+
+namespace {
+
+int fail(ppf_ctx* ctx, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  if (ctx) ctx->err = buf;
+  return code;
+}
+
+#define HIPCHK(ctx, expr)                                                              \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess)                                                              \
+      return fail(ctx, PPF_ERR_DEVICE, "%s failed: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+int ilog2_exact(int v) {
+  if (v <= 0 || (v & (v - 1))) return -1;
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  return l;
+}
+
+int check_nbin(ppf_ctx* ctx, int nbin, int* logN) {
+  const int l = ilog2_exact(nbin);
+  if (l < 6 || l > 13)
+    return fail(ctx, PPF_ERR_UNSUPPORTED, "nbin=%d: must be a power of two in [64, 8192]", nbin);
+  *logN = l - 1;  // complex FFT length N = nbin / 2
+  return PPF_OK;
+}
+
+int nharm_pad(int nbin) { return ((nbin / 2 + 1) + 7) & ~7; }
+
+// get_noise_PS: kc = int((1 - 1/4) * nharm) (pplib.py:2245)
+int noise_kc(int nbin) { return (int)(0.75 * (double)(nbin / 2 + 1)); }
+
+int ensure(ppf_ctx* ctx, Buffer& b, size_t bytes) {
+  if (b.bytes >= bytes) return PPF_OK;
+  if (b.p) {
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, hipFree(b.p));
+    b.p = nullptr;
+    b.bytes = 0;
+  }
+  if (hipMalloc(&b.p, bytes) != hipSuccess)
+    return fail(ctx, PPF_ERR_NOMEM, "hipMalloc(%zu) failed", bytes);
+  b.bytes = bytes;
+  return PPF_OK;
+}
+
+int twiddles(ppf_ctx* ctx, int nbin, const double2** out) {
+  const int l = ilog2_exact(nbin);
+  if (!ctx->tw[l]) {
+    HIPCHK(ctx, hipMalloc(&ctx->tw[l], (size_t)nbin * sizeof(double2)));
+    hipLaunchKernelGGL(k_twiddles, dim3((nbin + 255) / 256), dim3(256), 0, ctx->stream,
+                       ctx->tw[l], nbin);
+    HIPCHK(ctx, hipGetLastError());
+  }
+  *out = ctx->tw[l];
+  return PPF_OK;
+}
+
+hipEvent_t ev_get(ppf_ctx* ctx) {
+  if (!ctx->pool.empty()) {
+    hipEvent_t e = ctx->pool.back();
+    ctx->pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+// Launch helper: optional HIP-event bracket on the context stream.
+template <typename F>
+int timed(ppf_ctx* ctx, int kid, F&& launch) {
+  hipEvent_t a = nullptr, b = nullptr;
+  if (ctx->timing) {
+    a = ev_get(ctx);
+    b = ev_get(ctx);
+    HIPCHK(ctx, hipEventRecord(a, ctx->stream));
+  }
+  launch();
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(ctx, PPF_ERR_DEVICE, "kernel %d launch: %s", kid, hipGetErrorString(e));
+  if (ctx->timing) {
+    HIPCHK(ctx, hipEventRecord(b, ctx->stream));
+    ctx->pending.push_back({kid, a, b});
+  }
+  return PPF_OK;
+}
+
+int resolve_timing(ppf_ctx* ctx) {
+  for (auto& t : ctx->pending) {
+    HIPCHK(ctx, hipEventSynchronize(t.b));
+    float ms = 0.f;
+    HIPCHK(ctx, hipEventElapsedTime(&ms, t.a, t.b));
+    ctx->ktime[t.kid] += (double)ms;
+    ctx->klaunch[t.kid] += 1;
+    ctx->pool.push_back(t.a);
+    ctx->pool.push_back(t.b);
+  }
+  ctx->pending.clear();
+  return PPF_OK;
+}
+
+#define LOGN_SWITCH(L, BODY)                          \
+  switch (L) {                                        \
+    case 5: { constexpr int LG = 5; BODY; } break;    \
+    case 6: { constexpr int LG = 6; BODY; } break;    \
+    case 7: { constexpr int LG = 7; BODY; } break;    \
+    case 8: { constexpr int LG = 8; BODY; } break;    \
+    case 9: { constexpr int LG = 9; BODY; } break;    \
+    case 10: { constexpr int LG = 10; BODY; } break;  \
+    case 11: { constexpr int LG = 11; BODY; } break;  \
+    case 12: { constexpr int LG = 12; BODY; } break;  \
+    default: break;                                   \
+  }
+
+// Template spectra for nrow rows of nbin (DC zeroed when zero_dc).
+int model_spectra(ppf_ctx* ctx, int nrow, int nbin, const double* model, int zero_dc, Buffer& buf,
+                  double2** M, double** pn) {
+  int logN;
+  if (int r = check_nbin(ctx, nbin, &logN)) return r;
+  const int NHP = nharm_pad(nbin);
+  const size_t mbytes = (size_t)nrow * NHP * sizeof(double2);
+  const size_t pbytes = ((size_t)nrow * sizeof(double) + 255) & ~(size_t)255;
+  if (int r = ensure(ctx, buf, mbytes + pbytes)) return r;
+  *M = reinterpret_cast<double2*>(buf.p);
+  *pn = reinterpret_cast<double*>(static_cast<char*>(buf.p) + mbytes);
+  const double2* tw;
+  if (int r = twiddles(ctx, nbin, &tw)) return r;
+  double2* Mp = *M;
+  double* pp = *pn;
+  return timed(ctx, PPF_K_MODEL_FFT, [&] {
+    LOGN_SWITCH(logN, hipLaunchKernelGGL(k_model_spec<LG>, dim3(nrow), dim3(kBlock), 0,
+                                         ctx->stream, model, Mp, pp, NHP, zero_dc, tw));
+  });
+}
+
+size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+}  // namespace
+
+extern "C" {
+
+int ppf_version(void) { return PPF_VERSION; }
+
+int ppf_ctx_create(int device, ppf_ctx** out) {
+  if (!out) return PPF_ERR_INVALID;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return PPF_ERR_DEVICE;
+  if (device < 0 || device >= n) return PPF_ERR_INVALID;
+  if (hipSetDevice(device) != hipSuccess) return PPF_ERR_DEVICE;
+  ppf_ctx* c = new ppf_ctx();
+  c->device = device;
+  *out = c;
+  return PPF_OK;
+}
+
+void ppf_ctx_destroy(ppf_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  for (auto& t : ctx->pending) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
+  for (auto e : ctx->pool) (void)hipEventDestroy(e);
+  for (auto p : ctx->tw) if (p) (void)hipFree(p);
+  if (ctx->ws.p) (void)hipFree(ctx->ws.p);
+  if (ctx->mspec.p) (void)hipFree(ctx->mspec.p);
+  if (ctx->aux.p) (void)hipFree(ctx->aux.p);
+  delete ctx;
+}
+
+const char* ppf_last_error(const ppf_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int ppf_set_stream(ppf_ctx* ctx, void* stream) {
+  if (!ctx) return PPF_ERR_INVALID;
+  ctx->stream = reinterpret_cast<hipStream_t>(stream);
+  return PPF_OK;
+}
+
+int ppf_synchronize(ppf_ctx* ctx) {
+  if (!ctx) return PPF_ERR_INVALID;
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return PPF_OK;
+}
+
+int ppf_set_workspace_limit(ppf_ctx* ctx, int64_t bytes) {
+  if (!ctx || bytes <= 0) return PPF_ERR_INVALID;
+  ctx->ws_limit = bytes;
+  return PPF_OK;
+}
+
+int ppf_set_timing(ppf_ctx* ctx, int enable) {
+  if (!ctx) return PPF_ERR_INVALID;
+  ctx->timing = enable != 0;
+  return PPF_OK;
+}
+
+int ppf_get_kernel_time(ppf_ctx* ctx, int kid, double* total_ms, int64_t* launches) {
+  if (!ctx || kid < 0 || kid >= PPF_NUM_KERNELS) return PPF_ERR_INVALID;
+  if (int r = resolve_timing(ctx)) return r;
+  if (total_ms) *total_ms = ctx->ktime[kid];
+  if (launches) *launches = ctx->klaunch[kid];
+  return PPF_OK;
+}
+
+int ppf_reset_kernel_times(ppf_ctx* ctx) {
+  if (!ctx) return PPF_ERR_INVALID;
+  if (int r = resolve_timing(ctx)) return r;
+  for (int i = 0; i < PPF_NUM_KERNELS; ++i) { ctx->ktime[i] = 0.0; ctx->klaunch[i] = 0; }
+  return PPF_OK;
+}
+
+// ---------------------------------------------------------------------------
+int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_result* o) {
+  if (!ctx || !d || !o) return fail(ctx, PPF_ERR_INVALID, "null argument");
+  if (d->nsub <= 0) return PPF_OK;
+  if (d->nchan <= 0 || d->nchan > PPF_MAX_NCHAN)
+    return fail(ctx, PPF_ERR_UNSUPPORTED, "nchan=%d outside [1, %d]", d->nchan, PPF_MAX_NCHAN);
+  if (d->nmodel <= 0) return fail(ctx, PPF_ERR_INVALID, "nmodel must be >= 1");
+  if (d->method != PPF_METHOD_TRUST_NCG)
+    return fail(ctx, PPF_ERR_UNSUPPORTED, "Method %d is not implemented.", d->method);
+  if (!d->data || !d->model || !d->freqs || !d->P || !d->init || !d->nu_fit || !d->nu_out)
+    return fail(ctx, PPF_ERR_INVALID, "missing required input pointer");
+  if (!o->params || !o->param_errs || !o->nu_out || !o->cov || !o->scales || !o->scale_errs ||
+      !o->channel_snrs || !o->chi2 || !o->red_chi2 || !o->snr || !o->nfev || !o->status)
+    return fail(ctx, PPF_ERR_INVALID, "missing required output pointer");
+  if (d->guess && d->guess_Ns < 2) return fail(ctx, PPF_ERR_INVALID, "guess_Ns must be >= 2");
+  int logN;
+  if (int r = check_nbin(ctx, d->nbin, &logN)) return r;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  const int nchan = d->nchan, nbin = d->nbin;
+  const int NH = nbin / 2 + 1, NHP = nharm_pad(nbin);
+  const int kc = noise_kc(nbin);
+  const double2* tw;
+  if (int r = twiddles(ctx, nbin, &tw)) return r;
+  double2* M;
+  double* pn;
+  if (int r = model_spectra(ctx, d->nmodel * nchan, nbin, d->model, 1, ctx->mspec, &M, &pn))
+    return r;
+
+  // per-subint workspace layout
+  const size_t bX = (size_t)nchan * NHP * sizeof(double2);
+  const size_t bR = (size_t)NHP * sizeof(double2);
+  const size_t bC = (size_t)nchan * sizeof(double);
+  const size_t bAcc = (size_t)2 * nchan * 10 * sizeof(double);
+  const size_t bW = (size_t)nchan * 8 * sizeof(double);
+  const size_t per_sub = bX + 2 * bR + 2 * bC + sizeof(SolveState) + bAcc + bW;
+  int64_t chunk = ctx->ws_limit / (int64_t)(per_sub + 1024);
+  if (chunk < 1) chunk = 1;
+  if (chunk > d->nsub) chunk = d->nsub;
+  const size_t cs = (size_t)chunk;
+  const size_t offX = 0;
+  const size_t offR = align256(offX + cs * bX);
+  const size_t offMm = align256(offR + cs * bR);
+  const size_t offSig = align256(offMm + cs * bR);
+  const size_t offDs = align256(offSig + cs * bC);
+  const size_t offSt = align256(offDs + cs * bC);
+  const size_t offAcc = align256(offSt + cs * sizeof(SolveState));
+  const size_t offW = align256(offAcc + cs * bAcc);
+  const size_t total = align256(offW + cs * bW);
+  if (int r = ensure(ctx, ctx->ws, total)) return r;
+  char* base = static_cast<char*>(ctx->ws.p);
+
+  SpecArgs sa;
+  sa.nchan = nchan;
+  sa.NHP = NHP;
+  sa.kc = kc;
+  sa.guess = d->guess;
+  sa.data = d->data;
+  sa.M = M;
+  sa.model_idx = d->model_idx;
+  sa.freqs = d->freqs;
+  sa.errs = d->errs;
+  sa.mask = d->chan_mask;
+  sa.weights = d->weights;
+  sa.P = d->P;
+  sa.init = d->init;
+  sa.guess_nu = d->guess_nu;
+  sa.X = reinterpret_cast<double2*>(base + offX);
+  sa.R = reinterpret_cast<double2*>(base + offR);
+  sa.sig = reinterpret_cast<double*>(base + offSig);
+  sa.dsum = reinterpret_cast<double*>(base + offDs);
+  sa.tw = tw;
+
+  FitArgs fa;
+  fa.nchan = nchan;
+  fa.nbin = nbin;
+  fa.NH = NH;
+  fa.NHP = NHP;
+  fa.kc = kc;
+  for (int i = 0; i < 5; ++i) fa.flags[i] = d->fit_flags[i] ? 1 : 0;
+  fa.log10_tau = d->log10_tau;
+  fa.option = d->option;
+  fa.is_toa = d->is_toa;
+  fa.guess = d->guess;
+  fa.Ns = d->guess_Ns;
+  fa.guess_wrap = d->guess_wrap;
+  fa.X = sa.X;
+  fa.R = sa.R;
+  fa.M = M;
+  fa.pn = pn;
+  fa.model_idx = d->model_idx;
+  fa.sig = sa.sig;
+  fa.dsum = sa.dsum;
+  fa.freqs = d->freqs;
+  fa.mask = d->chan_mask;
+  fa.P = d->P;
+  fa.init = d->init;
+  fa.nu_fit = d->nu_fit;
+  fa.nu_out = d->nu_out;
+  fa.guess_nu = d->guess_nu;
+  fa.guess_tau = d->guess_tau;
+  fa.st = reinterpret_cast<SolveState*>(base + offSt);
+  fa.acc = reinterpret_cast<double*>(base + offAcc);
+  fa.wsc = reinterpret_cast<double*>(base + offW);
+  fa.o_params = o->params;
+  fa.o_param_errs = o->param_errs;
+  fa.o_nu_out = o->nu_out;
+  fa.o_cov = o->cov;
+  fa.o_scales = o->scales;
+  fa.o_scale_errs = o->scale_errs;
+  fa.o_channel_snrs = o->channel_snrs;
+  fa.o_chi2 = o->chi2;
+  fa.o_red_chi2 = o->red_chi2;
+  fa.o_snr = o->snr;
+  fa.o_nfev = o->nfev;
+  fa.o_status = o->status;
+  fa.o_init_used = o->init_used;
+  fa.o_fun = o->fun;
+  fa.o_cov_nosc = o->cov_nosc;
+
+  const size_t lds_meta = align256((size_t)nchan * (3 * sizeof(double) + sizeof(int)));
+  const size_t lds_guess = (size_t)NHP * sizeof(double2);
+  for (int64_t s0 = 0; s0 < d->nsub; s0 += chunk) {
+    const int nc = (int)std::min<int64_t>(chunk, d->nsub - s0);
+    sa.sub0 = (int)s0;
+    fa.sub0 = (int)s0;
+    if (int r = timed(ctx, PPF_K_DATA_XSPEC, [&] {
+          LOGN_SWITCH(logN, hipLaunchKernelGGL(k_data_xspec<LG>, dim3(nc), dim3(kBlock), 0,
+                                               ctx->stream, sa));
+        }))
+      return r;
+    if (int r = timed(ctx, PPF_K_FIT, [&] {
+          hipLaunchKernelGGL(k_guess, dim3(nc), dim3(kBlock), d->guess ? lds_guess : 0,
+                             ctx->stream, fa);
+        }))
+      return r;
+    // each subint runs in exactly one of the phase-only / scattering variants
+    if (int r = timed(ctx, PPF_K_FIT, [&] {
+          hipLaunchKernelGGL(k_solve<false>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
+          hipLaunchKernelGGL(k_solve<true>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
+        }))
+      return r;
+    if (int r = timed(ctx, PPF_K_FIT, [&] {
+          hipLaunchKernelGGL(k_post<false>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
+          hipLaunchKernelGGL(k_post<true>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
+        }))
+      return r;
+  }
+  return PPF_OK;
+}
+
+int ppf_phase_shift_batch(ppf_ctx* ctx, int32_t nprof, int32_t nbin, const double* data,
+                          const double* model, const int32_t* model_idx, const double* noise,
+                          int32_t Ns, double lo, double hi, double* out) {
+  if (!ctx || !data || !model || !out) return fail(ctx, PPF_ERR_INVALID, "null argument");
+  if (nprof <= 0) return PPF_OK;
+  if (Ns < 2) return fail(ctx, PPF_ERR_INVALID, "Ns must be >= 2");
+  int logN;
+  if (int r = check_nbin(ctx, nbin, &logN)) return r;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  // number of template rows = 1 + max(model_idx); the caller sizes model.
+  int nmodel = 1;
+  if (model_idx) {
+    std::vector<int32_t> h(nprof);
+    HIPCHK(ctx, hipMemcpyAsync(h.data(), model_idx, nprof * sizeof(int32_t), hipMemcpyDeviceToHost,
+                               ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    for (int32_t v : h) {
+      if (v < 0) return fail(ctx, PPF_ERR_INVALID, "negative model_idx");
+      nmodel = std::max(nmodel, (int)v + 1);
+    }
+  }
+  double2* M;
+  double* pn;
+  if (int r = model_spectra(ctx, nmodel, nbin, model, 1, ctx->aux, &M, &pn)) return r;
+  const double2* tw;
+  if (int r = twiddles(ctx, nbin, &tw)) return r;
+  PhaseShiftArgs pa;
+  pa.NHP = nharm_pad(nbin);
+  pa.kc = noise_kc(nbin);
+  pa.Ns = Ns;
+  pa.lo = lo;
+  pa.hi = hi;
+  pa.data = data;
+  pa.M = M;
+  pa.model_idx = model_idx;
+  pa.noise = noise;
+  pa.out = out;
+  pa.tw = tw;
+  return timed(ctx, PPF_K_PHASE_SHIFT, [&] {
+    LOGN_SWITCH(logN, hipLaunchKernelGGL(k_phase_shift<LG>, dim3(nprof), dim3(kBlock), 0,
+                                         ctx->stream, pa));
+  });
+}
+
+int ppf_rotate_rows(ppf_ctx* ctx, int32_t nrow, int32_t nbin, const double* in,
+                    const double* phase, double* out) {
+  if (!ctx || !in || !phase || !out) return fail(ctx, PPF_ERR_INVALID, "null argument");
+  if (nrow <= 0) return PPF_OK;
+  int logN;
+  if (int r = check_nbin(ctx, nbin, &logN)) return r;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  const double2* tw;
+  if (int r = twiddles(ctx, nbin, &tw)) return r;
+  return timed(ctx, PPF_K_ROTATE, [&] {
+    LOGN_SWITCH(logN, hipLaunchKernelGGL(k_rotate_rows<LG>, dim3(nrow), dim3(kBlock), 0,
+                                         ctx->stream, in, phase, out, tw));
+  });
+}
+
+int ppf_irfft_rows(ppf_ctx* ctx, int32_t nrow, int32_t nbin, const double* spec, double* out) {
+  if (!ctx || !spec || !out) return fail(ctx, PPF_ERR_INVALID, "null argument");
+  if (nrow <= 0) return PPF_OK;
+  int logN;
+  if (int r = check_nbin(ctx, nbin, &logN)) return r;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  const double2* tw;
+  if (int r = twiddles(ctx, nbin, &tw)) return r;
+  const double2* sp = reinterpret_cast<const double2*>(spec);
+  return timed(ctx, PPF_K_IRFFT, [&] {
+    LOGN_SWITCH(logN, hipLaunchKernelGGL(k_irfft_rows<LG>, dim3(nrow), dim3(kBlock), 0,
+                                         ctx->stream, sp, out, tw));
+  });
+}
+
+int ppf_noise_rows(ppf_ctx* ctx, int32_t nrow, int32_t nbin, const double* in, double* out) {
+  if (!ctx || !in || !out) return fail(ctx, PPF_ERR_INVALID, "null argument");
+  if (nrow <= 0) return PPF_OK;
+  int logN;
+  if (int r = check_nbin(ctx, nbin, &logN)) return r;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  const double2* tw;
+  if (int r = twiddles(ctx, nbin, &tw)) return r;
+  const int kc = noise_kc(nbin);
+  return timed(ctx, PPF_K_NOISE, [&] {
+    LOGN_SWITCH(logN, hipLaunchKernelGGL(k_noise_rows<LG>, dim3(nrow), dim3(kBlock), 0,
+                                         ctx->stream, in, out, kc, tw));
+  });
+}
+
+int ppf_synth_portraits(ppf_ctx* ctx, int32_t nsub, int32_t nchan, int32_t nbin,
+                        const double* model, const double* phase, double sigma, uint64_t seed,
+                        int64_t sub0, double* data) {
+  if (!ctx || !model || !phase || !data) return fail(ctx, PPF_ERR_INVALID, "null argument");
+  if (nsub <= 0 || nchan <= 0) return PPF_OK;
+  int logN;
+  if (int r = check_nbin(ctx, nbin, &logN)) return r;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  double2* M;
+  double* pn;
+  if (int r = model_spectra(ctx, nchan, nbin, model, 0, ctx->aux, &M, &pn)) return r;
+  const double2* tw;
+  if (int r = twiddles(ctx, nbin, &tw)) return r;
+  const int NHP = nharm_pad(nbin);
+  const int64_t rows = (int64_t)nsub * nchan;
+  if (rows > 0x7fffffff) return fail(ctx, PPF_ERR_INVALID, "too many rows");
+  return timed(ctx, PPF_K_SYNTH, [&] {
+    LOGN_SWITCH(logN, hipLaunchKernelGGL(k_synth<LG>, dim3((unsigned)rows), dim3(kBlock), 0,
+                                         ctx->stream, M, phase, data, nchan, NHP, sigma, seed,
+                                         sub0, tw));
+  });
+}
+
+int ppf_rotate_accumulate(ppf_ctx* ctx, int32_t nsub, int32_t nchan, int32_t nbin,
+                          const double* data, const double* phase, const double* weight,
+                          double* accum) {
+  if (!ctx || !data || !phase || !weight || !accum)
+    return fail(ctx, PPF_ERR_INVALID, "null argument");
+  if (nsub <= 0 || nchan <= 0) return PPF_OK;
+  int logN;
+  if (int r = check_nbin(ctx, nbin, &logN)) return r;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  const double2* tw;
+  if (int r = twiddles(ctx, nbin, &tw)) return r;
+  const int NH = nbin / 2 + 1;
+  int nsplit = (2048 + nchan - 1) / nchan;
+  if (nsplit > nsub) nsplit = nsub;
+  if (nsplit < 1) nsplit = 1;
+  const size_t count = (size_t)nchan * NH;
+  if (int r = ensure(ctx, ctx->aux, (size_t)nsplit * count * sizeof(double2))) return r;
+  double2* partial = reinterpret_cast<double2*>(ctx->aux.p);
+  if (int r = timed(ctx, PPF_K_ROT_ACCUM, [&] {
+        LOGN_SWITCH(logN, hipLaunchKernelGGL(k_rot_accum<LG>, dim3(nsplit * nchan), dim3(kBlock),
+                                             0, ctx->stream, data, phase, weight, partial, nsub,
+                                             nchan, nsplit, tw));
+      }))
+    return r;
+  double2* acc = reinterpret_cast<double2*>(accum);
+  return timed(ctx, PPF_K_ROT_ACCUM, [&] {
+    hipLaunchKernelGGL(k_accum_reduce, dim3((unsigned)((count + 255) / 256)), dim3(256), 0,
+                       ctx->stream, partial, acc, nsplit, count);
+  });
+}
+
+}  // extern "C"

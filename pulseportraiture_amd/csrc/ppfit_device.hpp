@@ -1,0 +1,212 @@
+// ppfit_device.hpp -- device-side building blocks for libppfit (gfx950).
+//
+// Complex fp64 helpers, 64-lane wave reductions, a Philox4x32-10 counter RNG
+// and the LDS-resident Stockham FFT used for every real<->complex transform
+// on the hot path (numpy.fft.rfft / irfft in the reference: pplib.py:27).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ppf {
+
+// pplib.py:48-51: Dconst = 0.000241**-1 (bit-identical double)
+constexpr double kDconst = 0x1.03560a9f560aap+12;
+constexpr double kPi = 3.141592653589793116;
+constexpr double kLn10 = 0x1.26bb1bbb55516p+1;
+constexpr int kBlock = 256;   // threads per workgroup (4 waves)
+constexpr int kWaves = kBlock / 64;
+
+__device__ __forceinline__ double2 cmk(double x, double y) { return make_double2(x, y); }
+__device__ __forceinline__ double2 cadd(double2 a, double2 b) { return cmk(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double2 csub(double2 a, double2 b) { return cmk(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ double2 cscale(double2 a, double s) { return cmk(a.x * s, a.y * s); }
+__device__ __forceinline__ double2 cconj(double2 a) { return cmk(a.x, -a.y); }
+__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+  return cmk(fma(a.x, b.x, -a.y * b.y), fma(a.x, b.y, a.y * b.x));
+}
+// a * conj(b)
+__device__ __forceinline__ double2 cmulc(double2 a, double2 b) {
+  return cmk(fma(a.x, b.x, a.y * b.y), fma(a.y, b.x, -a.x * b.y));
+}
+__device__ __forceinline__ double cabs2(double2 a) { return fma(a.x, a.x, a.y * a.y); }
+
+// e^{2 pi i k phi} with the argument reduced exactly: k*phi is split into
+// its rounded product and the FMA remainder, the integer part is dropped, and
+// sincospi evaluates the fractional turn (no large-argument rounding, unlike
+// exp(2j*pi*outer(phi,k)) in pptoaslib.py:237, which is within 1e-11 of this).
+__device__ __forceinline__ double2 turn_phasor(double k, double phi) {
+  double t = k * phi;
+  double e = fma(k, phi, -t);
+  double r = (t - rint(t)) + e;
+  double s, c;
+  sincospi(2.0 * r, &s, &c);
+  return cmk(c, s);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// Sum over the 8 lanes that share (lane >> 3): xor 1, 2, 4.
+__device__ __forceinline__ double group8_sum(double v) {
+  v += __shfl_xor(v, 1);
+  v += __shfl_xor(v, 2);
+  v += __shfl_xor(v, 4);
+  return v;
+}
+
+// Block-wide sum; `red` is >= kWaves doubles of LDS.  Every thread gets it.
+__device__ __forceinline__ double block_sum(double v, double* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  double s = 0.0;
+#pragma unroll
+  for (int i = 0; i < kWaves; ++i) s += red[i];
+  __syncthreads();
+  return s;
+}
+
+// ---------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al. 2011): counter-based, so CPU and GPU can
+// regenerate identical uniform streams for the synthetic inputs.
+// ---------------------------------------------------------------------------
+struct u32x4 { uint32_t v[4]; };
+
+__device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint64_t p0 = (uint64_t)0xD2511F53u * c.v[0];
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * c.v[2];
+    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    u32x4 n;
+    n.v[0] = hi1 ^ c.v[1] ^ k0;
+    n.v[1] = lo1;
+    n.v[2] = hi0 ^ c.v[3] ^ k1;
+    n.v[3] = lo0;
+    c = n;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// Two N(0,1) deviates (Box-Muller) from one Philox block.
+__device__ __forceinline__ double2 philox_normal2(u32x4 c, uint64_t seed) {
+  u32x4 x = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  const double inv53 = 1.1102230246251565404e-16;  // 2^-53
+  double u1 = ((double)(x.v[0] >> 5) * 67108864.0 + (double)(x.v[1] >> 6) + 0.5) * inv53;
+  double u2 = ((double)(x.v[2] >> 5) * 67108864.0 + (double)(x.v[3] >> 6)) * inv53;
+  double r = sqrt(-2.0 * log(u1));
+  double s, co;
+  sincospi(2.0 * u2, &s, &co);
+  return cmk(r * co, r * s);
+}
+
+// ---------------------------------------------------------------------------
+// LDS Stockham autosort FFT of N = 2^LOGN complex points, all kBlock threads.
+// tw[m] = exp(-2 pi i m / (2N)), m in [0, 2N), built by k_twiddles.
+// Forward uses exp(-i...), INV the conjugate (unnormalised both ways).
+// Radix-2 first pass when LOGN is odd, then radix-4 passes.
+// ---------------------------------------------------------------------------
+template <bool INV>
+__device__ __forceinline__ void radix4(double2& a0, double2& a1, double2& a2, double2& a3) {
+  double2 t0 = cadd(a0, a2), t1 = csub(a0, a2);
+  double2 t2 = cadd(a1, a3), d = csub(a1, a3);
+  double2 t3 = INV ? cmk(-d.y, d.x) : cmk(d.y, -d.x);  // (+/-i)(a1-a3)
+  a0 = cadd(t0, t2);
+  a1 = cadd(t1, t3);
+  a2 = csub(t0, t2);
+  a3 = csub(t1, t3);
+}
+
+template <int LOGN, bool INV>
+__device__ void lds_fft(double2* buf, const double2* __restrict__ tw) {
+  constexpr int N = 1 << LOGN;
+  constexpr int Q = N / 4;
+  constexpr int B4 = (Q + kBlock - 1) / kBlock;
+  const int tid = threadIdx.x;
+  int Ns = 1;
+  if constexpr (LOGN & 1) {
+    constexpr int H = N / 2;
+    constexpr int B2 = (H + kBlock - 1) / kBlock;
+    double2 a[B2], b[B2];
+#pragma unroll
+    for (int c = 0; c < B2; ++c) {
+      const int j = tid + c * kBlock;
+      if (j < H) { a[c] = buf[j]; b[c] = buf[j + H]; }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < B2; ++c) {
+      const int j = tid + c * kBlock;
+      if (j < H) { buf[2 * j] = cadd(a[c], b[c]); buf[2 * j + 1] = csub(a[c], b[c]); }
+    }
+    __syncthreads();
+    Ns = 2;
+  }
+#pragma unroll
+  for (int p = 0; p < LOGN / 2; ++p) {
+    double2 v[B4][4];
+#pragma unroll
+    for (int c = 0; c < B4; ++c) {
+      const int j = tid + c * kBlock;
+      if (j < Q) {
+        const int k = j & (Ns - 1);
+        const int tstep = 2 * k * (N / (4 * Ns));
+        v[c][0] = buf[j];
+#pragma unroll
+        for (int r = 1; r < 4; ++r) {
+          double2 w = tw[r * tstep];
+          if (INV) w.y = -w.y;
+          v[c][r] = cmul(buf[j + r * Q], w);
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < B4; ++c) {
+      const int j = tid + c * kBlock;
+      if (j < Q) {
+        radix4<INV>(v[c][0], v[c][1], v[c][2], v[c][3]);
+        const int k = j & (Ns - 1);
+        const int d = (j - k) * 4 + k;
+        buf[d] = v[c][0];
+        buf[d + Ns] = v[c][1];
+        buf[d + 2 * Ns] = v[c][2];
+        buf[d + 3 * Ns] = v[c][3];
+      }
+    }
+    __syncthreads();
+    Ns *= 4;
+  }
+}
+
+// Real-input spectrum X_k (k in [0, N]) of the 2N-point real row packed as
+// buf[j] = (x_{2j}, x_{2j+1}) after a forward lds_fft (numpy rfft layout).
+template <int LOGN>
+__device__ __forceinline__ double2 rfft_post(const double2* buf, int k, const double2* __restrict__ tw) {
+  constexpr int N = 1 << LOGN;
+  const double2 zk = buf[k & (N - 1)];
+  const double2 zc = cconj(buf[(N - k) & (N - 1)]);
+  const double2 e = cscale(cadd(zk, zc), 0.5);
+  const double2 dd = csub(zk, zc);
+  const double2 o = cmk(0.5 * dd.y, -0.5 * dd.x);  // -i/2 (zk - zc)
+  return cadd(e, cmul(tw[k], o));
+}
+
+// Packed spectrum Z_k (k in [0, N)) for the inverse: irfft(X) = (1/N) *
+// unpack(IFFT_N(Z)).  Imaginary parts of X_0 and X_N are ignored (pocketfft c2r).
+template <int LOGN>
+__device__ __forceinline__ double2 irfft_pre(double2 xk, double2 xnk, int k, const double2* __restrict__ tw) {
+  const double2 xc = cconj(xnk);
+  const double2 e = cscale(cadd(xk, xc), 0.5);
+  const double2 o = cmul(cscale(csub(xk, xc), 0.5), cconj(tw[k]));
+  return cmk(e.x - o.y, e.y + o.x);  // e + i o
+}
+
+}  // namespace ppf

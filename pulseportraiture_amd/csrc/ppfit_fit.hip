@@ -1,0 +1,1116 @@
+// ppfit_fit.hip -- the batched wideband fit (kernels (c), (d), (e) of SURVEY.md §8).
+//
+// One workgroup owns one subint for the whole fit and re-reads that subint's
+// cross-spectrum X (written once by k_data_xspec) on every objective pass.
+//   k_guess : initial phase of get_TOAs / ppalign (pptoas.py:420-456,
+//             ppalign.py:180-185) -- FFTFIT brute force + Nelder-Mead.
+//   k_solve : scipy trust-ncg (gtol=-1, pptoaslib.py:1001-1014) with Steihaug
+//             CG, every pass one fused sweep giving f, g and H
+//             (pptoaslib.py:525-643).
+//   k_post  : zero-covariance frequencies (pptoaslib.py:733-906), phi/tau at
+//             nu_out (1040-1065), the with-scales Hessian and its Woodbury
+//             inverse (645-731, 1069-1077), snr and chi2 (1079-1085).
+//
+// Cell-pass lane layout: a wave holds 8 channels x 8 harmonic phases; lane
+// (g, h) walks k = h, h+8, ... of channel g with the phasor advanced by the
+// angle-addition recurrence and re-seeded exactly every 32 steps, so one
+// wave load instruction covers 8 full 128-byte segments of X.
+#include "ppfit_kernels.hpp"
+
+namespace ppf {
+
+constexpr int NACC = 10;
+constexpr double kTwoPi = 2.0 * kPi;
+constexpr double kFourPi2 = 4.0 * kPi * kPi;
+constexpr double kDconst2 = kDconst * kDconst;  // Dconst**2
+
+// upper-triangle pair p -> (i, j); compile-time so unrolled loops index
+// ChanDeriv members statically (a runtime index would push it to scratch)
+__host__ __device__ constexpr int pair_i(int p) {
+  return p < 5 ? 0 : (p < 9 ? 1 : (p < 12 ? 2 : (p < 14 ? 3 : 4)));
+}
+__host__ __device__ constexpr int pair_j(int p) {
+  return p < 5 ? p : (p < 9 ? p - 4 : (p < 12 ? p - 7 : (p < 14 ? p - 9 : 4)));
+}
+
+// ---------------------------------------------------------------------------
+// per-subint channel metadata in LDS
+// ---------------------------------------------------------------------------
+struct Meta {
+  int* chan;    // ok-channel ordinal -> channel index
+  double* fr;   // frequency
+  double* iw2;  // 1 / errs_FT^2, errs_FT = sigma sqrt(nbin/2) (pptoaslib.py:980-984)
+  double* pn;   // sum_{k>=1} |M_nk|^2 (Sbp with tau = 0)
+  int nok;
+};
+
+__device__ __forceinline__ size_t meta_bytes(int nchan) {
+  return (size_t)nchan * (3 * sizeof(double) + sizeof(int));
+}
+
+__device__ Meta load_meta(const FitArgs& a, int c, int s, unsigned char* dyn, int* s_nok) {
+  Meta m;
+  const int nchan = a.nchan;
+  m.fr = reinterpret_cast<double*>(dyn);
+  m.iw2 = m.fr + nchan;
+  m.pn = m.iw2 + nchan;
+  m.chan = reinterpret_cast<int*>(m.pn + nchan);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint8_t* mask = a.mask ? a.mask + (size_t)s * nchan : nullptr;
+  if (tid < 64) {
+    int base = 0;
+    for (int n0 = 0; n0 < nchan; n0 += 64) {
+      const int n = n0 + lane;
+      const bool ok = n < nchan && (!mask || mask[n]);
+      const unsigned long long b = __ballot(ok);
+      const int rank = __popcll(b & ((1ull << lane) - 1ull));
+      if (ok) m.chan[base + rank] = n;
+      base += __popcll(b);
+    }
+    if (lane == 0) *s_nok = base;
+  }
+  __syncthreads();
+  m.nok = *s_nok;
+  const int midx = a.model_idx ? a.model_idx[s] : 0;
+  const double half = 0.5 * (double)a.nbin;
+  for (int j = tid; j < m.nok; j += kBlock) {
+    const int n = m.chan[j];
+    m.fr[j] = a.freqs[(size_t)s * nchan + n];
+    const double sg = a.sig[(size_t)c * nchan + n];
+    m.iw2[j] = 1.0 / (sg * sg * half);
+    m.pn[j] = a.pn[(size_t)midx * nchan + n];
+  }
+  __syncthreads();
+  return m;
+}
+
+// Python's float % 1.0 (CPython float_rem): result in [0, 1).
+__device__ __forceinline__ double pymod1(double x) {
+  double r = fmod(x, 1.0);
+  if (r != 0.0) {
+    if (r < 0.0) r += 1.0;
+  } else {
+    r = 0.0;
+  }
+  return r;
+}
+
+// phase_transform(..., mod=True) wrap, pplib.py:2610-2613
+__device__ __forceinline__ double wrap_half(double p) {
+  if (fabs(p) >= 0.5) p = pymod1(p);
+  if (p >= 0.5) p -= 1.0;
+  return p;
+}
+
+// Sum N values over the block; result valid in all threads.
+template <int N>
+__device__ __forceinline__ void block_sum_vec(double (&v)[N], double (*red)[48]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const double t = wave_sum(v[i]);
+    if (lane == 0) red[w][i] = t;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    double t = 0.0;
+    for (int q = 0; q < kWaves; ++q) t += red[q][i];
+    v[i] = t;
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// Cell sweeps over one channel row of X (lane's harmonics k = h + 8 j)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void cells_phase(const double2* __restrict__ Xr, int J, int h,
+                                            double phif, double* acc) {
+  const double2 step = turn_phasor(8.0, phif);
+  double2 e = cmk(1.0, 0.0);
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+  for (int j = 0; j < J; ++j) {
+    const int k = h + 8 * j;
+    if ((j & 31) == 0) e = turn_phasor((double)k, phif);
+    else e = cmul(e, step);
+    const double2 x = Xr[k];
+    const double wr = fma(x.x, e.x, -x.y * e.y);
+    const double wi = fma(x.x, e.y, x.y * e.x);
+    const double kd = (double)k;
+    a0 += wr;
+    a1 = fma(kd, wi, a1);
+    a2 = fma(kd * kd, wr, a2);
+  }
+  acc[0] = a0; acc[1] = a1; acc[2] = a2;
+  for (int i = 3; i < NACC; ++i) acc[i] = 0.0;
+}
+
+// With scattering: B = 1/(1 + 2 pi i k tau_n), f = B(B-1)/tau_n and
+// g1 = 2 B (B-1)^2 / tau_n^2 give every tau/alpha derivative of B through a
+// per-channel real factor (pptoaslib.py:318-356).
+__device__ __forceinline__ void cells_scat(const double2* __restrict__ Xr,
+                                           const double2* __restrict__ Mr, int J, int h,
+                                           double phif, double taun, double* acc) {
+  const double2 step = turn_phasor(8.0, phif);
+  const double itau = 1.0 / taun;
+  const double w0 = kTwoPi * taun;
+  double2 e = cmk(1.0, 0.0);
+  double a[NACC];
+  for (int i = 0; i < NACC; ++i) a[i] = 0.0;
+  for (int j = 0; j < J; ++j) {
+    const int k = h + 8 * j;
+    if ((j & 31) == 0) e = turn_phasor((double)k, phif);
+    else e = cmul(e, step);
+    const double2 x = Xr[k];
+    const double2 mm = Mr[k];
+    const double m2 = cabs2(mm);
+    const double2 W = cmul(x, e);
+    const double kd = (double)k;
+    const double aa = w0 * kd;
+    const double id = 1.0 / fma(aa, aa, 1.0);
+    const double2 B = cmk(id, -aa * id);
+    const double2 Bm1 = cmk(B.x - 1.0, B.y);
+    const double2 f = cscale(cmul(B, Bm1), itau);
+    const double2 g1 = cscale(cmul(f, Bm1), 2.0 * itau);
+    const double2 WB = cmulc(W, B);
+    const double2 Wf = cmulc(W, f);
+    const double2 Wg = cmulc(W, g1);
+    a[0] += WB.x;
+    a[1] = fma(kd, WB.y, a[1]);
+    a[2] = fma(kd * kd, WB.x, a[2]);
+    a[3] += Wf.x;
+    a[4] = fma(kd, Wf.y, a[4]);
+    a[5] += Wg.x;
+    a[6] = fma(cabs2(B), m2, a[6]);
+    a[7] = fma(fma(B.x, f.x, B.y * f.y), m2, a[7]);
+    a[8] = fma(cabs2(f), m2, a[8]);
+    a[9] = fma(fma(B.x, g1.x, B.y * g1.y), m2, a[9]);
+  }
+  for (int i = 0; i < NACC; ++i) acc[i] = a[i];
+}
+
+// ---------------------------------------------------------------------------
+// Per-channel derived terms: C_n, its phase/scattering derivatives, S_n and
+// its derivatives, all divided by errs_FT^2 (pptoaslib.py:390-523).
+// ---------------------------------------------------------------------------
+struct ChanDeriv {
+  double C, C1, C2, F1, F1p, G1, S, SF, SFF, SG;
+  double dph[3];   // d phi_n / d(phi, DM, GM)          pptoaslib.py:216-225
+  double dts[2];   // d tau_n / d(tau, alpha)            pptoaslib.py:246-257
+  double d2ts[3];  // tau-tau, tau-alpha, alpha-alpha    pptoaslib.py:259-274
+};
+
+template <bool SCAT>
+__device__ __forceinline__ ChanDeriv derive(const double* acc, bool scat, double pn, double iw2,
+                                            double fr, const double* prm, double tau_lin,
+                                            const double* refs, double P, bool log10_tau) {
+  ChanDeriv d;
+  d.C = acc[0] * iw2;
+  d.C1 = -kTwoPi * acc[1] * iw2;
+  d.C2 = -kFourPi2 * acc[2] * iw2;
+  if (SCAT && scat) {
+    d.F1 = acc[3] * iw2;
+    d.F1p = -kTwoPi * acc[4] * iw2;
+    d.G1 = acc[5] * iw2;
+    d.S = acc[6] * iw2;
+    d.SF = acc[7] * iw2;
+    d.SFF = acc[8] * iw2;
+    d.SG = acc[9] * iw2;
+  } else {
+    d.F1 = d.F1p = d.G1 = d.SF = d.SFF = d.SG = 0.0;
+    d.S = pn * iw2;
+  }
+  const double f2 = 1.0 / (fr * fr), f4 = f2 * f2;
+  const double r0 = 1.0 / (refs[0] * refs[0]);
+  const double r1 = 1.0 / (refs[1] * refs[1]);
+  d.dph[0] = 1.0;
+  d.dph[1] = kDconst * (f2 - r0) / P;
+  d.dph[2] = kDconst2 * (f4 - r1 * r1) / P;
+  if (!SCAT) {
+    d.dts[0] = d.dts[1] = 0.0;
+    d.d2ts[0] = d.d2ts[1] = d.d2ts[2] = 0.0;
+    return d;
+  }
+  const double ratio = fr / refs[2];
+  const double taus = tau_lin * pow(ratio, prm[4]);
+  const double lnr = log(ratio);
+  const bool has = tau_lin != 0.0;
+  if (!log10_tau) {
+    d.dts[0] = has ? taus / tau_lin : 0.0;
+    d.dts[1] = lnr * taus;
+    d.d2ts[0] = 0.0;
+    d.d2ts[1] = has ? d.dts[1] / tau_lin : 0.0;
+  } else {
+    d.dts[0] = kLn10 * taus;
+    d.dts[1] = lnr * taus;
+    d.d2ts[0] = kLn10 * d.dts[0];
+    d.d2ts[1] = kLn10 * d.dts[1];
+  }
+  d.d2ts[2] = lnr * d.dts[1];
+  return d;
+}
+
+__device__ __forceinline__ double dC_(const ChanDeriv& d, int i) {
+  return i < 3 ? d.C1 * d.dph[i] : d.dts[i - 3] * d.F1;
+}
+__device__ __forceinline__ double dS_(const ChanDeriv& d, int i) {
+  return i < 3 ? 0.0 : 2.0 * d.dts[i - 3] * d.SF;
+}
+__device__ __forceinline__ double d2ts_(const ChanDeriv& d, int i, int j) {
+  return (i == 0 && j == 0) ? d.d2ts[0] : ((i == 1 && j == 1) ? d.d2ts[2] : d.d2ts[1]);
+}
+__device__ __forceinline__ double d2C_(const ChanDeriv& d, int i, int j) {
+  if (i < 3 && j < 3) return d.C2 * d.dph[i] * d.dph[j];
+  if (i < 3) return d.dph[i] * d.dts[j - 3] * d.F1p;
+  if (j < 3) return d.dph[j] * d.dts[i - 3] * d.F1p;
+  return d.dts[i - 3] * d.dts[j - 3] * d.G1 + d2ts_(d, i - 3, j - 3) * d.F1;
+}
+__device__ __forceinline__ double d2S_(const ChanDeriv& d, int i, int j) {
+  if (i < 3 || j < 3) return 0.0;
+  return 2.0 * (d.dts[i - 3] * d.dts[j - 3] * (d.SFF + d.SG) + d2ts_(d, i - 3, j - 3) * d.SF);
+}
+// Hij_n of pptoaslib.py:624-628 (unmasked)
+__device__ __forceinline__ double Hn_(const ChanDeriv& d, int i, int j) {
+  const double C = d.C, S = d.S;
+  const double dCi = dC_(d, i), dCj = dC_(d, j), dSi = dS_(d, i), dSj = dS_(d, j);
+  return -2.0 * (C * C / S) *
+         ((d2C_(d, i, j) / C) - (0.5 * d2S_(d, i, j) / S) + (dCi * dCj / (C * C)) +
+          (dSi * dSj / (S * S)) - ((dCi * dSj) + (dSi * dCj)) / (C * S));
+}
+
+// phi_n (pptoaslib.py:206-208), reduced to [0, 1)
+__device__ __forceinline__ double phase_frac(const double* prm, double fr, const double* refs,
+                                             double P) {
+  const double f2 = 1.0 / (fr * fr);
+  const double r0 = 1.0 / (refs[0] * refs[0]);
+  const double r1 = 1.0 / (refs[1] * refs[1]);
+  const double ph = prm[0] + kDconst * prm[1] * (f2 - r0) / P +
+                    kDconst2 * prm[2] * (f2 * f2 - r1 * r1) / P;
+  return ph - floor(ph);
+}
+
+// One sweep over all fitted channels at (prm, refs).  MODE 0: f, g, H for
+// the solver (out[0..20]) and raw accumulators into acc_slot; MODE 1: the
+// with-scales Hessian pieces (out[0..29]) and per-channel wsc rows.  SCAT
+// compiles the scattering cell loop in; without it tau must be 0 (host-side
+// dispatch guarantees it), which keeps the phase-only kernels lean.
+// Each 8-channel group's contributions are reduced across the wave at once
+// and added into the wave's own LDS row, so nothing is carried through the
+// cell loop in registers.
+template <int MODE, bool SCAT>
+__device__ void sweep(const FitArgs& a, const Meta& m, int c, int s, const double* prm,
+                      const double* refs, double P, double* acc_slot, double* out,
+                      double (*red)[48]) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g8 = lane >> 3, h = lane & 7;
+  const int J = a.NHP >> 3;
+  const bool log10_tau = a.log10_tau != 0;
+  const double tau_lin = SCAT ? (log10_tau ? pow(10.0, prm[3]) : prm[3]) : 0.0;
+  const bool scat = SCAT && tau_lin != 0.0;
+  const int midx = a.model_idx ? a.model_idx[s] : 0;
+  constexpr int NP = MODE == 0 ? 21 : 45;
+  if (lane < NP) red[w][lane] = 0.0;
+  __syncthreads();
+  const int ngroups = (m.nok + 7) >> 3;
+  for (int gi = w; gi < ngroups; gi += kWaves) {
+    const int j = gi * 8 + g8;
+    const bool valid = j < m.nok;
+    const int jj = valid ? j : m.nok - 1;
+    const int n = m.chan[jj];
+    const double fr = m.fr[jj];
+    const double phif = phase_frac(prm, fr, refs, P);
+    const double2* Xr = a.X + ((size_t)c * a.nchan + n) * a.NHP;
+    double acc[NACC];
+    if (!scat) {
+      cells_phase(Xr, J, h, phif, acc);
+    } else {
+      const double2* Mr = a.M + ((size_t)midx * a.nchan + n) * a.NHP;
+      const double taun = tau_lin * pow(fr / refs[2], prm[4]);
+      cells_scat(Xr, Mr, J, h, phif, taun, acc);
+    }
+#pragma unroll
+    for (int i = 0; i < NACC; ++i) acc[i] = group8_sum(acc[i]);
+    double ct[NP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) ct[i] = 0.0;
+    if (h == 0 && valid) {
+      const ChanDeriv d = derive<SCAT>(acc, scat, m.pn[j], m.iw2[j], fr, prm, tau_lin, refs, P,
+                                       log10_tau);
+      const double q = d.C * d.C / d.S;
+      if (MODE == 0) {
+        double* dst = acc_slot + (size_t)j * NACC;
+        for (int i = 0; i < NACC; ++i) dst[i] = acc[i];
+        ct[0] = -q;
+#pragma unroll
+        for (int i = 0; i < 5; ++i)
+          if (a.flags[i]) ct[1 + i] = -q * (2.0 * dC_(d, i) / d.C - dS_(d, i) / d.S);
+#pragma unroll
+                for (int p = 0; p < 15; ++p) {
+          const int pi = pair_i(p), pj = pair_j(p);
+          if (a.flags[pi] && a.flags[pj]) ct[6 + p] = Hn_(d, pi, pj);
+        }
+      } else {
+        const double sc = d.C / d.S;
+        double cross[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) cross[i] = -2.0 * (dC_(d, i) - sc * dS_(d, i));
+        double* dst = a.wsc + ((size_t)c * a.nchan + j) * 8;
+        dst[0] = sc;
+        dst[1] = d.S;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) dst[2 + i] = cross[i];
+        const double ic = 1.0 / (2.0 * d.S);
+#pragma unroll
+                for (int p = 0; p < 15; ++p) {
+          const int pi = pair_i(p), pj = pair_j(p);
+          if (a.flags[pi] && a.flags[pj]) {
+            ct[p] = -2.0 * q * ((d2C_(d, pi, pj) / d.C) - (0.5 * d2S_(d, pi, pj) / d.S));
+            ct[15 + p] = cross[pi] * cross[pj] * ic;
+            ct[30 + p] = Hn_(d, pi, pj);  // curvature without amplitude terms
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      double v = ct[i];
+      v += __shfl_xor(v, 8);
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      if (lane == 0) red[w][i] += v;
+    }
+  }
+  __syncthreads();
+  if (tid < NP) {
+    double t = 0.0;
+    for (int q = 0; q < kWaves; ++q) t += red[q][tid];
+    out[tid] = t;
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// k_guess
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_guess(FitArgs a) {
+  extern __shared__ __align__(16) unsigned char dyn[];
+  __shared__ GuessShared gs;
+  __shared__ double s_v[4];
+  const int c = blockIdx.x, s = a.sub0 + c, tid = threadIdx.x;
+  const int nchan = a.nchan;
+  const uint8_t* mask = a.mask ? a.mask + (size_t)s * nchan : nullptr;
+  double fsum = 0.0, cnt = 0.0;
+  for (int n = tid; n < nchan; n += kBlock)
+    if (!mask || mask[n]) { fsum += a.freqs[(size_t)s * nchan + n]; cnt += 1.0; }
+  fsum = block_sum(fsum, gs.red);
+  cnt = block_sum(cnt, gs.red);
+  const double fmean = fsum / cnt;
+  SolveState& st = a.st[c];
+  if (tid == 0) {
+    for (int i = 0; i < 5; ++i) st.x[i] = a.init[(size_t)s * 5 + i];
+    for (int i = 0; i < 3; ++i) {
+      const double v = a.nu_fit[(size_t)s * 3 + i];
+      st.refs[i] = isnan(v) ? fmean : v;
+    }
+    st.nfev = 0;
+    st.status = -1;
+    st.slot = 0;
+    st.fun = NAN;
+    const double tl = a.log10_tau ? pow(10.0, st.x[3]) : st.x[3];
+    st.scat = (tl != 0.0) || a.flags[3];
+    st.scat_post = st.scat;
+  }
+  if (!a.guess) {
+    __syncthreads();
+    if (tid == 0) for (int i = 0; i < 5; ++i) st.init[i] = st.x[i];
+    return;
+  }
+  // rm_k = R_k conj(Mm_k B_k(tau_g)): the guess template is irfft(B rfft(mean
+  // model)) when a scattering guess is given (pptoas.py:441-446).
+  double2* rm = reinterpret_cast<double2*>(dyn);
+  const double2* Rr = a.R + (size_t)c * a.NHP;
+  const double tg = a.guess_tau ? a.guess_tau[s] : 0.0;
+  const int N = a.NH - 1;
+  const int midx = a.model_idx ? a.model_idx[s] : 0;
+  const double2* Mb = a.M + (size_t)midx * nchan * a.NHP;
+  const double inv_cnt = 1.0 / cnt;
+  double pno = 0.0;
+  for (int k = tid; k < a.NH; k += kBlock) {
+    const double2 r = Rr[k];
+    // modelx.mean(axis=0) over the fitted channels (pptoas.py:454); its
+    // spectrum is the mean of the DC-zeroed channel spectra.
+    double2 mm = cmk(0.0, 0.0);
+    for (int n = 0; n < nchan; ++n)
+      if (!mask || mask[n]) mm = cadd(mm, Mb[(size_t)n * a.NHP + k]);
+    mm = cscale(mm, inv_cnt);
+    if (k == N) mm.y = 0.0;
+    if (tg != 0.0) {
+      const double aa = kTwoPi * (double)k * tg;
+      const double id = 1.0 / fma(aa, aa, 1.0);
+      mm = cmul(mm, cmk(id, -aa * id));
+      if (k == N) mm.y = 0.0;
+    }
+    rm[k] = cmulc(r, mm);
+    if (k >= a.kc) pno += cabs2(r);
+  }
+  pno = block_sum(pno, gs.red);  // includes the barrier that publishes rm
+  // err = get_noise(rot_prof) * sqrt(nbin/2), pplib.py:2076-2080
+  const double noise = sqrt(pno / (double)a.nbin / (double)(a.NH - a.kc));
+  const double err2 = noise * noise * (0.5 * (double)a.nbin);
+  guess_search(rm, a.NH, 1.0 / err2, a.Ns, -0.5, 0.5, gs);
+  if (tid == 0) {
+    double nug = a.guess_nu ? a.guess_nu[s] : NAN;
+    if (isnan(nug)) nug = fmean;
+    const double P = a.P[s];
+    const double DM = st.x[1];
+    double phi = gs.x;
+    // phase_transform(phi, DM_guess, nu_g, nu_fit_DM, P, mod), pplib.py:2609
+    phi = phi + (kDconst * DM * (1.0 / P) *
+                 (pow(st.refs[0], -2.0) - pow(nug, -2.0)));
+    if (a.guess_wrap) phi = wrap_half(phi);
+    st.x[0] = phi;
+    for (int i = 0; i < 5; ++i) st.init[i] = st.x[i];
+  }
+  (void)s_v;
+}
+
+// ---------------------------------------------------------------------------
+// k_solve: scipy.optimize._trustregion._minimize_trust_region with the
+// CGSteihaugSubproblem (scipy 1.15, _trustregion.py / _trustregion_ncg.py):
+// initial radius 1, max 1000, eta 0.15, gtol -1, maxiter 200 * 5.
+// ---------------------------------------------------------------------------
+// The 5-parameter trust-region step runs on wave 0 with lane i < 5 holding
+// component i of every vector (lanes >= 5 hold zeros): dot products are an
+// 8-lane shuffle sum broadcast from lane 0, H.v gathers v by lane shuffles.
+// Every lane then runs the same scalar control flow, so the step needs a few
+// registers per lane instead of dozens of 5-vectors on one thread.
+__device__ __forceinline__ double dot8(double a, double b) {
+  double v = a * b;
+  v += __shfl_xor(v, 1);
+  v += __shfl_xor(v, 2);
+  v += __shfl_xor(v, 4);
+  return __shfl(v, 0);
+}
+__device__ __forceinline__ double hvec(const double (&Hrow)[5], double v) {
+  double s = 0.0;
+#pragma unroll
+  for (int j = 0; j < 5; ++j) s += Hrow[j] * __shfl(v, j);
+  return s;
+}
+// m(p) = f + g.p + 0.5 p.(H p)   (BaseQuadraticSubproblem.__call__)
+__device__ __forceinline__ double model_val(double f, double g, const double (&Hrow)[5], double p) {
+  return f + dot8(g, p) + 0.5 * dot8(p, hvec(Hrow, p));
+}
+// get_boundaries_intersections: ||z + t d|| = tr, sorted roots
+__device__ __forceinline__ void boundary_t(double z, double d, double tr, double& ta, double& tb) {
+  const double a = dot8(d, d), b = 2.0 * dot8(z, d), c = dot8(z, z) - tr * tr;
+  const double sq = sqrt(b * b - 4.0 * a * c);
+  const double aux = b + copysign(sq, b);
+  double t1 = -aux / (2.0 * a), t2 = -2.0 * c / aux;
+  if (t1 > t2) { const double t = t1; t1 = t2; t2 = t; }
+  ta = t1;
+  tb = t2;
+}
+
+// CG-Steihaug, Nocedal & Wright alg. 7.2 as in scipy's CGSteihaugSubproblem.
+// Returns this lane's component of the step p.
+__device__ __forceinline__ double steihaug(double f, double g, const double (&Hrow)[5], double tr,
+                                           int& hits) {
+  const double jm = sqrt(dot8(g, g));
+  const double tol = fmin(0.5, sqrt(jm)) * jm;
+  if (jm < tol) { hits = 0; return 0.0; }
+  double z = 0.0, r = g, d = -g;
+  for (int it = 0; it < 64; ++it) {
+    const double Bd = hvec(Hrow, d);
+    const double dBd = dot8(d, Bd);
+    if (dBd <= 0.0) {
+      double ta, tb;
+      boundary_t(z, d, tr, ta, tb);
+      const double pa = z + ta * d, pb = z + tb * d;
+      hits = 1;
+      return model_val(f, g, Hrow, pa) < model_val(f, g, Hrow, pb) ? pa : pb;
+    }
+    const double r2 = dot8(r, r);
+    const double alpha = r2 / dBd;
+    const double zn = z + alpha * d;
+    if (sqrt(dot8(zn, zn)) >= tr) {
+      double ta, tb;
+      boundary_t(z, d, tr, ta, tb);
+      hits = 1;
+      return z + tb * d;
+    }
+    const double rn = r + alpha * Bd;
+    const double rn2 = dot8(rn, rn);
+    if (sqrt(rn2) < tol) { hits = 0; return zn; }
+    const double beta = rn2 / r2;
+    d = -rn + beta * d;
+    z = zn;
+    r = rn;
+  }
+  hits = 0;  // a 5-D CG ends well before this
+  return z;
+}
+
+struct SolveShared {
+  double x[5], xp[5];
+  double out[48];
+  double red[kWaves][48];
+  int done, nok;
+};
+
+template <bool SCAT>
+__global__ __launch_bounds__(kBlock) void k_solve(FitArgs a) {
+  extern __shared__ __align__(16) unsigned char dyn[];
+  __shared__ SolveShared sh;
+  __shared__ double refs[3];
+  const int c = blockIdx.x, s = a.sub0 + c, tid = threadIdx.x;
+  const int lane = tid & 63;
+  if ((a.st[c].scat != 0) != SCAT) return;  // the other variant owns this subint
+  const Meta m = load_meta(a, c, s, dyn, &sh.nok);
+  SolveState& st = a.st[c];
+  const double P = a.P[s];
+  if (tid < 5) sh.x[tid] = st.x[tid];
+  if (tid < 3) refs[tid] = st.refs[tid];
+  if (tid == 0) sh.done = (m.nok == 0);
+  __syncthreads();
+  double* acc0 = a.acc + (size_t)c * 2 * a.nchan * NACC;
+  // wave-0 solver state (lane i < 5 owns component i; scalars are uniform)
+  double f = 0.0, g = 0.0, xl = 0.0, Hrow[5] = {0, 0, 0, 0, 0};
+  double tr = 1.0, predv = 0.0, pl = 0.0;
+  int hits = 0, k = 0, status = (m.nok == 0) ? -1 : 0, nfev = 0, slot = 0;
+  auto load_fgh = [&](double& ff, double& gg, double (&HH)[5]) {
+    ff = sh.out[0];
+    gg = lane < 5 ? sh.out[1 + lane] : 0.0;
+#pragma unroll
+    for (int p = 0; p < 15; ++p) {
+      const double v = sh.out[6 + p];
+      if (lane == pair_i(p)) HH[pair_j(p)] = v;
+      if (lane == pair_j(p)) HH[pair_i(p)] = v;
+    }
+  };
+  if (!sh.done) {
+    sweep<0, SCAT>(a, m, c, s, sh.x, refs, P, acc0, sh.out, sh.red);
+    if (tid < 64) {
+      load_fgh(f, g, Hrow);
+      xl = lane < 5 ? sh.x[lane] : 0.0;
+      nfev = 1;
+    }
+  }
+  while (!sh.done) {
+    if (tid < 64) {
+      const double jm = sqrt(dot8(g, g));
+      if (!(jm >= -1.0)) {  // NaN gradient: scipy's loop condition fails
+        status = 0;
+        if (lane == 0) sh.done = 1;
+      } else {
+        pl = steihaug(f, g, Hrow, tr, hits);
+        predv = model_val(f, g, Hrow, pl);
+        if (lane < 5) sh.xp[lane] = xl + pl;
+      }
+    }
+    __syncthreads();
+    if (sh.done) break;
+    double* sl = acc0 + (size_t)(slot ^ 1) * a.nchan * NACC;
+    sweep<0, SCAT>(a, m, c, s, sh.xp, refs, P, sl, sh.out, sh.red);
+    if (tid < 64) {
+      double fp, gp, Hp[5] = {0, 0, 0, 0, 0};
+      load_fgh(fp, gp, Hp);
+      nfev += 1;
+      const double actual = f - fp;
+      const double pred = f - predv;
+      if (pred <= 0.0) {
+        status = 2;
+        if (lane == 0) sh.done = 1;
+      } else {
+        const double rho = actual / pred;
+        if (rho < 0.25) tr *= 0.25;
+        else if (rho > 0.75 && hits) tr = fmin(2.0 * tr, 1000.0);
+        if (rho > 0.15) {
+          xl = xl + pl;
+          f = fp;
+          g = gp;
+#pragma unroll
+          for (int j = 0; j < 5; ++j) Hrow[j] = Hp[j];
+          slot ^= 1;
+          if (lane < 5) sh.x[lane] = xl;
+        }
+        k += 1;
+        if (k >= 1000) {
+          status = 1;
+          if (lane == 0) sh.done = 1;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (tid < 5) st.x[tid] = sh.x[tid];
+  if (tid == 0) {
+    st.fun = m.nok ? f : NAN;
+    st.nfev = m.nok ? nfev : 0;
+    st.status = status;
+    st.slot = slot;
+    const double tl = a.log10_tau ? pow(10.0, sh.x[3]) : sh.x[3];
+    st.scat_post = SCAT && tl != 0.0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_post
+// ---------------------------------------------------------------------------
+// Real roots of sum_i c[i] y^(deg-i) (deg <= 6) in ascending order: the roots
+// of the derivative bracket them; each bracket is bisected to convergence.
+__device__ int poly_real_roots(const double* cin, int deg, double* roots) {
+  double c[7];
+  int off = 0;
+  while (off <= deg && cin[off] == 0.0) ++off;  // np.roots strips leading zeros
+  int d = deg - off;
+  for (int i = 0; i <= d; ++i) c[i] = cin[off + i];
+  while (d > 0 && c[d] == 0.0) --d;             // trailing zeros: roots at 0 (not > 0)
+  if (d <= 0) return 0;
+  double pol[7][7];
+  for (int i = 0; i <= d; ++i) pol[d][i] = c[i] / c[0];
+  for (int o = d - 1; o >= 1; --o)
+    for (int i = 0; i <= o; ++i) pol[o][i] = pol[o + 1][i] * (double)(o + 1 - i) / (double)(o + 1);
+  double bound = 0.0;
+  for (int i = 1; i <= d; ++i) bound = fmax(bound, fabs(pol[d][i]));
+  bound = 1.0 + bound;
+  double prev[7];
+  int np_ = 1;
+  prev[0] = -pol[1][1];  // linear
+  for (int o = 2; o <= d; ++o) {
+    double pts[9];
+    int npts = 0;
+    pts[npts++] = -bound;
+    for (int i = 0; i < np_; ++i) pts[npts++] = fmin(fmax(prev[i], -bound), bound);
+    pts[npts++] = bound;
+    double cur[7];
+    int nc = 0;
+    auto ev = [&](double x) {
+      double v = pol[o][0];
+      for (int i = 1; i <= o; ++i) v = v * x + pol[o][i];
+      return v;
+    };
+    for (int q = 0; q + 1 < npts; ++q) {
+      double lo = pts[q], hi = pts[q + 1];
+      double flo = ev(lo), fhi = ev(hi);
+      if (flo == 0.0) { if (nc == 0 || cur[nc - 1] != lo) cur[nc++] = lo; continue; }
+      if ((flo < 0.0) == (fhi < 0.0)) continue;
+      for (int it = 0; it < 200; ++it) {
+        const double mid = 0.5 * (lo + hi);
+        if (mid == lo || mid == hi) break;
+        const double fm = ev(mid);
+        if ((fm < 0.0) == (flo < 0.0)) { lo = mid; flo = fm; } else { hi = mid; }
+      }
+      cur[nc++] = 0.5 * (lo + hi);
+    }
+    if (ev(bound) == 0.0) cur[nc++] = bound;
+    np_ = nc;
+    for (int i = 0; i < nc; ++i) prev[i] = cur[i];
+  }
+  for (int i = 0; i < np_; ++i) roots[i] = prev[i];
+  return np_;
+}
+
+// Gauss-Jordan inverse with partial pivoting (np.linalg.inv), n <= 5.
+__device__ bool invert_small(const double* A, int n, double* Ai) {
+  double M[5][10];
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < 2 * n; ++j) M[i][j] = j < n ? A[i * n + j] : (j - n == i ? 1.0 : 0.0);
+  for (int col = 0; col < n; ++col) {
+    int piv = col;
+    for (int r = col + 1; r < n; ++r)
+      if (fabs(M[r][col]) > fabs(M[piv][col])) piv = r;
+    if (M[piv][col] == 0.0) return false;
+    if (piv != col)
+      for (int j = 0; j < 2 * n; ++j) { const double t = M[col][j]; M[col][j] = M[piv][j]; M[piv][j] = t; }
+    const double iv = 1.0 / M[col][col];
+    for (int j = 0; j < 2 * n; ++j) M[col][j] *= iv;
+    for (int r = 0; r < n; ++r) {
+      if (r == col) continue;
+      const double fct = M[r][col];
+      if (fct == 0.0) continue;
+      for (int j = 0; j < 2 * n; ++j) M[r][j] -= fct * M[col][j];
+    }
+  }
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) Ai[i * n + j] = M[i][j + n];
+  return true;
+}
+
+// Per-channel contributions to the zero-covariance sums (pptoaslib.py:746-901).
+// Returns the number of sums; the branch id is chosen by the caller.
+enum { NZ_NONE = 0, NZ_PD, NZ_PG, NZ_TA, NZ_PDT, NZ_PDG, NZ_PDTA, NZ_PDGT };
+
+__device__ __forceinline__ int nz_branch(const int* ff) {
+  const int code = ff[0] * 16 + ff[1] * 8 + ff[2] * 4 + ff[3] * 2 + ff[4];
+  switch (code) {
+    case 0b11000: return NZ_PD;
+    case 0b10100: return NZ_PG;
+    case 0b00011: return NZ_TA;
+    case 0b11010: return NZ_PDT;
+    case 0b11100: return NZ_PDG;
+    case 0b11011: return NZ_PDTA;
+    case 0b11111: return NZ_PDTA;  // approximated with [1,1,0,1,1] (pptoaslib.py:893-901)
+    case 0b11110: return NZ_PDGT;
+    default: return NZ_NONE;
+  }
+}
+
+__device__ void nz_terms(int br, int option, const ChanDeriv& d, double fr, const double* refs,
+                         const int* fl, double* t) {
+  const double f2 = 1.0 / (fr * fr), f4 = f2 * f2, lnf = log(fr);
+  auto H = [&](int i, int j) { return (fl[i] && fl[j]) ? Hn_(d, i, j) : 0.0; };
+  for (int i = 0; i < 22; ++i) t[i] = 0.0;
+  switch (br) {
+    case NZ_PD: {
+      const double h = H(1, 0) / d.dph[1];
+      t[0] = f2 * h; t[1] = h;
+    } break;
+    case NZ_PG: {
+      const double h = H(0, 2) / d.dph[2];
+      t[0] = f4 * h; t[1] = h;
+    } break;
+    case NZ_TA: {
+      // taus_deriv[1] / taus = ln(fr / nu_tau)
+      const double h = H(3, 4) / log(fr / refs[2]);
+      t[0] = lnf * h; t[1] = h;
+    } break;
+    case NZ_PDT: {
+      const double h21 = H(1, 0) / d.dph[1], h23 = H(1, 3) / d.dph[1];
+      t[0] = f2 * h23; t[1] = f2 * h21; t[2] = h23; t[3] = h21; t[4] = H(3, 0); t[5] = H(3, 3);
+    } break;
+    case NZ_PDG: {
+      if (option == 0) {
+        const double h21 = H(1, 0) / d.dph[1], h23 = H(1, 2) / d.dph[1];
+        const double h31 = H(2, 0) / d.dph[2], h33 = H(2, 2) / d.dph[2];
+        t[0] = h31 * f4; t[1] = h31; t[2] = h23 * f2; t[3] = h23;
+        t[4] = h33 * f4; t[5] = h33; t[6] = h21 * f2; t[7] = h21;
+      } else if (option == 1) {
+        const double h21 = H(1, 0) / d.dph[1], h22 = H(1, 1) / d.dph[1];
+        const double h31 = H(2, 0) / d.dph[2], h32 = H(2, 1) / d.dph[2];
+        t[0] = h21 * f4; t[1] = h21; t[2] = h32 * f2; t[3] = h32;
+        t[4] = h22 * f4; t[5] = h22; t[6] = h31 * f2; t[7] = h31;
+      }
+    } break;
+    case NZ_PDTA: {
+      const double lr = log(fr / refs[2]);
+      const double h21 = H(1, 0) / d.dph[1], h23 = H(1, 3) / d.dph[1], h24 = H(1, 4) / d.dph[1];
+      const double h41 = H(4, 0) / lr, h42 = H(4, 1) / lr, h43 = H(4, 3) / lr;
+      t[0] = f2 * h21; t[1] = f2 * h23; t[2] = f2 * h24;
+      t[3] = h21; t[4] = h23; t[5] = h24;
+      t[6] = lnf * h41; t[7] = lnf * h42; t[8] = lnf * h43;
+      t[9] = h41; t[10] = h42; t[11] = h43;
+      t[12] = H(0, 0); t[13] = H(1, 1); t[14] = H(3, 3); t[15] = H(4, 4);
+      t[16] = H(0, 1); t[17] = H(0, 3); t[18] = H(0, 4); t[19] = H(1, 3); t[20] = H(1, 4);
+      t[21] = H(3, 4);
+    } break;
+    case NZ_PDGT: {
+      const double g2 = f2 - 1.0 / (refs[0] * refs[0]);
+      const double r1 = 1.0 / (refs[1] * refs[1]);
+      const double g4 = f4 - r1 * r1;
+      if (option == 0) {
+        const double h21 = H(1, 0) / g2, h23 = H(1, 2) / g2, h24 = H(1, 3) / g2;
+        const double h31 = H(2, 0) / g4, h33 = H(2, 2) / g4, h34 = H(2, 3) / g4;
+        t[0] = f4 * h34; t[1] = h34; t[2] = f2 * h21; t[3] = h21; t[4] = f4 * h31; t[5] = h31;
+        t[6] = f2 * h23; t[7] = h23; t[8] = f4 * h33; t[9] = h33; t[10] = f2 * h24; t[11] = h24;
+      } else if (option == 1) {
+        const double h21 = H(1, 0) / g2, h22 = H(1, 1) / g2, h24 = H(1, 3) / g2;
+        const double h31 = H(2, 0) / g4, h32 = H(2, 1) / g4, h34 = H(2, 3) / g4;
+        t[0] = f2 * h24; t[1] = h24; t[2] = f4 * h31; t[3] = h31; t[4] = f2 * h21; t[5] = h21;
+        t[6] = f4 * h32; t[7] = h32; t[8] = f2 * h22; t[9] = h22; t[10] = f4 * h34; t[11] = h34;
+      }
+      t[12] = H(3, 0); t[13] = H(3, 3);
+    } break;
+    default: break;
+  }
+}
+
+__device__ double closest_positive(const double* coeffs, int deg, bool sq, double fmean) {
+  double r[7];
+  const int nr = poly_real_roots(coeffs, deg, r);
+  double best = NAN, bd = INFINITY;
+  for (int i = 0; i < nr; ++i) {
+    if (!(r[i] > 0.0)) continue;
+    const double x = sq ? sqrt(r[i]) : r[i];
+    const double dd = fabs(fmean - x);
+    if (dd < bd) { bd = dd; best = x; }
+  }
+  return best;
+}
+
+// Solve the branch from the channel sums t[22]; writes nz[3] (refs preset).
+__device__ void nz_solve(int br, int option, const double* t, double fmean, double* nz) {
+  switch (br) {
+    case NZ_PD: nz[0] = pow(t[0] / t[1], -0.5); break;
+    case NZ_PG: nz[1] = pow(t[0] / t[1], -0.25); break;
+    case NZ_TA: nz[2] = exp(t[0] / t[1]); break;
+    case NZ_PDT: {
+      const double num = t[4] * t[0] - t[5] * t[1];
+      const double den = t[4] * t[2] - t[5] * t[3];
+      nz[0] = pow(num / den, -0.5);
+    } break;
+    case NZ_PDG: {
+      if (option == 0 || option == 1) {
+        const double A = t[0], B = t[1], C = t[2], D = t[3], E = t[4], F = t[5], G = t[6],
+                     Hh = t[7];
+        // coeffs [A C - E G, 0, E H - A D, 0, F G - B C, 0, B D - F H] in nu:
+        // a cubic in y = nu^2 (pptoaslib.py:789-794)
+        const double cy[4] = {A * C - E * G, E * Hh - A * D, F * G - B * C, B * D - F * Hh};
+        const double x = closest_positive(cy, 3, true, fmean);
+        nz[0] = nz[1] = x;
+      }
+    } break;
+    case NZ_PDTA: {
+      const double H11 = t[12], H22 = t[13], H33 = t[14], H44 = t[15], H12 = t[16], H13 = t[17],
+                   H14 = t[18], H23 = t[19], H24 = t[20], H34 = t[21];
+      const double a1 = H34 * H34 - H33 * H44, a2 = H13 * H44 - H14 * H34,
+                   a3 = H14 * H33 - H13 * H34;
+      nz[0] = pow((a1 * t[0] + a2 * t[1] + a3 * t[2]) / (a1 * t[3] + a2 * t[4] + a3 * t[5]), -0.5);
+      const double b1 = H13 * H22 - H12 * H23, b2 = H11 * H23 - H12 * H13,
+                   b3 = H12 * H12 - H11 * H22;
+      nz[2] = exp((b1 * t[6] + b2 * t[7] + b3 * t[8]) / (b1 * t[9] + b2 * t[10] + b3 * t[11]));
+    } break;
+    case NZ_PDGT: {
+      if (option == 0 || option == 1) {
+        const double A = t[0], a = t[1], B = t[2], b = t[3], C = t[4], c = t[5], D = t[6],
+                     d = t[7], E = t[8], e = t[9], F = t[10], f = t[11], H14 = t[12],
+                     H44 = t[13];
+        double co[6];
+        int deg;
+        if (option == 0) {
+          co[0] = A * A * B + H44 * C * D + H14 * E * F - H44 * B * E - A * C * F - H14 * A * D;
+          co[1] = -A * A * b - H44 * C * d - H14 * E * f + H44 * b * E + A * C * f + H14 * A * d;
+          co[2] = -2 * A * a * B - H44 * c * D - H14 * e * F + H44 * B * e + (A * c + a * C) * F +
+                  H14 * a * D;
+          co[3] = 2 * A * a * b + H44 * c * d + H14 * e * f - H44 * b * e - (A * c + a * C) * f -
+                  H14 * a * d;
+          co[4] = a * a * B - a * c * F;
+          co[5] = -a * a * b + a * c * f;
+          deg = 5;
+        } else {
+          co[0] = A * A * B + H44 * C * D + H14 * E * F - H44 * B * E - A * C * F - H14 * A * D;
+          co[1] = -2 * A * a * B - H44 * c * D - H14 * e * F + H44 * B * e + (A * c + a * C) * F +
+                  H14 * a * D;
+          co[2] = -(A * A * b - a * a * B) - H44 * C * d - H14 * E * f + H44 * b * E +
+                  (A * C * f - a * c * F) + H14 * A * d;
+          co[3] = 2 * A * a * b + H44 * c * d + H14 * e * f - H44 * b * e - (A * c + a * C) * f -
+                  H14 * a * d;
+          co[4] = -a * a * b + a * c * f;
+          deg = 4;
+        }
+        const double x = closest_positive(co, deg, true, fmean);
+        nz[0] = nz[1] = x;
+      }
+    } break;
+    default: break;
+  }
+}
+
+struct PostShared {
+  double prm[5], refs[3], nu[3];
+  double out[48];
+  double red[kWaves][48];
+  double Xinv[25];
+  int ifit[5];
+  int nfit, nok, bad;
+  double fmean, Sd;
+};
+
+template <bool SCAT>
+__global__ __launch_bounds__(kBlock) void k_post(FitArgs a) {
+  extern __shared__ __align__(16) unsigned char dyn[];
+  __shared__ PostShared sh;
+  const int c = blockIdx.x, s = a.sub0 + c, tid = threadIdx.x;
+  if ((a.st[c].scat_post != 0) != SCAT) return;
+  const int nchan = a.nchan;
+  const Meta m = load_meta(a, c, s, dyn, &sh.nok);
+  const SolveState& st = a.st[c];
+  const double P = a.P[s];
+  const bool log10_tau = a.log10_tau != 0;
+  // zero the per-channel outputs of masked channels
+  if (a.mask) {
+    for (int n = tid; n < nchan; n += kBlock) {
+      if (a.mask[(size_t)s * nchan + n]) continue;
+      const size_t o = (size_t)s * nchan + n;
+      a.o_scales[o] = 0.0;
+      a.o_scale_errs[o] = 0.0;
+      a.o_channel_snrs[o] = 0.0;
+    }
+  }
+  // Sd (pptoaslib.py:985) and mean frequency of the fitted channels
+  {
+    double v[2] = {0.0, 0.0};
+    for (int j = tid; j < m.nok; j += kBlock) {
+      v[0] += a.dsum[(size_t)c * nchan + m.chan[j]] * m.iw2[j];
+      v[1] += m.fr[j];
+    }
+    block_sum_vec(v, sh.red);
+    if (tid == 0) { sh.Sd = v[0]; sh.fmean = v[1] / (double)m.nok; }
+  }
+  if (tid == 0) {
+    sh.nfit = 0;
+    for (int i = 0; i < 5; ++i) if (a.flags[i]) sh.ifit[sh.nfit++] = i;
+    for (int i = 0; i < 3; ++i) sh.refs[i] = st.refs[i];
+    sh.bad = (m.nok == 0);
+  }
+  __syncthreads();
+  if (sh.bad) {
+    if (tid == 0) {
+      for (int i = 0; i < 5; ++i) {
+        a.o_params[(size_t)s * 5 + i] = NAN;
+        a.o_param_errs[(size_t)s * 5 + i] = NAN;
+      }
+      a.o_status[s] = -1;
+      a.o_nfev[s] = 0;
+    }
+    return;
+  }
+  // ---- nu_out: given values, else zero-covariance frequencies ----
+  const double* acc_fin = a.acc + ((size_t)c * 2 + st.slot) * nchan * NACC;
+  bool need = false;
+  double nuo[3];
+  for (int i = 0; i < 3; ++i) {
+    nuo[i] = a.nu_out[(size_t)s * 3 + i];
+    if (isnan(nuo[i]) || nuo[i] == 0.0) need = true;
+  }
+  if (need) {
+    int fl[5];
+    for (int i = 0; i < 5; ++i) fl[i] = a.flags[i] ? 1 : 0;
+    const int br = nz_branch(fl);
+    if (br == NZ_PDTA) fl[2] = 0;  // [1,1,1,1,1] -> [1,1,0,1,1]
+    double t[22];
+    double sums[22];
+    for (int i = 0; i < 22; ++i) sums[i] = 0.0;
+    if (br != NZ_NONE) {
+      const double tau_lin = log10_tau ? pow(10.0, st.x[3]) : st.x[3];
+      const bool scat = SCAT && tau_lin != 0.0;
+      for (int j = tid; j < m.nok; j += kBlock) {
+        const ChanDeriv d = derive<SCAT>(acc_fin + (size_t)j * NACC, scat, m.pn[j], m.iw2[j], m.fr[j],
+                                   st.x, tau_lin, sh.refs, P, log10_tau);
+        nz_terms(br, a.option, d, m.fr[j], sh.refs, fl, t);
+        for (int i = 0; i < 22; ++i) sums[i] += t[i];
+      }
+    }
+    block_sum_vec(sums, sh.red);
+    if (tid == 0) {
+      double nz[3] = {sh.refs[0], sh.refs[1], sh.refs[2]};
+      nz_solve(br, a.option, sums, sh.fmean, nz);
+      for (int i = 0; i < 3; ++i) if (isnan(nuo[i])) nuo[i] = nz[i];
+    }
+  }
+  if (tid == 0) {
+    if (a.is_toa) {  // pptoaslib.py:1048-1050
+      if (a.flags[1]) nuo[1] = nuo[0];
+      else if (a.flags[2]) nuo[0] = nuo[1];
+    }
+    const double* x = st.x;
+    // phi at nu_out (pptoaslib.py:1052-1057)
+    const double phi_inf = x[0] + kDconst * x[1] * (0.0 - 1.0 / (sh.refs[0] * sh.refs[0])) / P +
+                           kDconst2 * x[2] *
+                               (0.0 - 1.0 / (sh.refs[1] * sh.refs[1] * sh.refs[1] * sh.refs[1])) / P;
+    double phi_out = phi_inf + ((kDconst / P) * x[1] * pow(nuo[0], -2.0)) +
+                     ((kDconst2 / P) * x[2] * pow(nuo[1], -4.0));
+    if (fabs(phi_out) >= 0.5) phi_out = pymod1(phi_out);
+    if (phi_out >= 0.5) phi_out -= 1.0;
+    // tau at nu_out (pptoaslib.py:1059-1065)
+    const double tau_fit = log10_tau ? pow(10.0, x[3]) : x[3];
+    double tau_out = tau_fit * pow(nuo[2] / sh.refs[2], x[4]);
+    if (log10_tau) tau_out = log10(tau_out);
+    sh.prm[0] = phi_out;
+    sh.prm[1] = x[1];
+    sh.prm[2] = x[2];
+    sh.prm[3] = tau_out;
+    sh.prm[4] = x[4];
+    for (int i = 0; i < 3; ++i) sh.nu[i] = nuo[i];
+  }
+  __syncthreads();
+  // ---- with-scales Hessian at the output parameters ----
+  sweep<1, SCAT>(a, m, c, s, sh.prm, sh.nu, P, nullptr, sh.out, sh.red);
+  if (tid == 0) {
+    const int nf = sh.nfit;
+    double A[25];
+    #pragma unroll
+    for (int p = 0; p < 15; ++p) {
+      const int pi = pair_i(p), pj = pair_j(p);
+      int ii = -1, jj = -1;
+      for (int q = 0; q < nf; ++q) { if (sh.ifit[q] == pi) ii = q; if (sh.ifit[q] == pj) jj = q; }
+      if (ii < 0 || jj < 0) continue;
+      const double v = sh.out[p] - sh.out[15 + p];  // A - U C^-1 V
+      A[ii * nf + jj] = v;
+      A[jj * nf + ii] = v;
+    }
+    if (!invert_small(A, nf, sh.Xinv))
+      for (int i = 0; i < nf * nf; ++i) sh.Xinv[i] = NAN;
+    if (a.o_cov_nosc) {
+      for (int p = 0; p < 15; ++p) {
+        const int pi = pair_i(p), pj = pair_j(p);
+        int ii = -1, jj = -1;
+        for (int q = 0; q < nf; ++q) { if (sh.ifit[q] == pi) ii = q; if (sh.ifit[q] == pj) jj = q; }
+        if (ii < 0 || jj < 0) continue;
+        A[ii * nf + jj] = A[jj * nf + ii] = 0.5 * sh.out[30 + p];
+      }
+      double Ci[25];
+      if (!invert_small(A, nf, Ci))
+        for (int i = 0; i < nf * nf; ++i) Ci[i] = NAN;
+      double* cn = a.o_cov_nosc + (size_t)s * 25;
+      for (int i = 0; i < 25; ++i) cn[i] = 0.0;
+      for (int q = 0; q < nf; ++q)
+        for (int r = 0; r < nf; ++r) cn[q * 5 + r] = Ci[q * nf + r];
+    }
+  }
+  __syncthreads();
+  // ---- per-channel amplitude errors and S/N (pptoaslib.py:717-724, 1079-1082) ----
+  const int nf = sh.nfit;
+  double snr2 = 0.0;
+  for (int j = tid; j < m.nok; j += kBlock) {
+    const double* w = a.wsc + ((size_t)c * nchan + j) * 8;
+    const double sc = w[0], S = w[1];
+    const double ic = 1.0 / (2.0 * S);
+    double LL[5], U[5];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) U[q] = q < nf ? w[2 + sh.ifit[q]] : 0.0;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+      double t = 0.0;
+#pragma unroll
+      for (int i = 0; i < 5; ++i)
+        if (i < nf && q < nf) t += U[i] * sh.Xinv[i * nf + q];
+      LL[q] = -ic * t;
+    }
+    double t = 0.0;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) t += LL[q] * U[q];
+    const double LR = -t * ic + ic;
+    const double csnr = sc * sqrt(S);
+    const int n = m.chan[j];
+    const size_t o = (size_t)s * nchan + n;
+    a.o_scales[o] = sc;
+    a.o_scale_errs[o] = sqrt(2.0 * LR);
+    a.o_channel_snrs[o] = csnr;
+    snr2 += csnr * csnr;
+  }
+  snr2 = block_sum(snr2, sh.red[0]);
+  if (tid == 0) {
+    double* op = a.o_params + (size_t)s * 5;
+    double* oe = a.o_param_errs + (size_t)s * 5;
+    for (int i = 0; i < 5; ++i) { op[i] = sh.prm[i]; oe[i] = 0.0; }
+    double* cv = a.o_cov + (size_t)s * 25;
+    for (int i = 0; i < 25; ++i) cv[i] = 0.0;
+    for (int q = 0; q < nf; ++q) {
+      oe[sh.ifit[q]] = sqrt(2.0 * sh.Xinv[q * nf + q]);
+      for (int r = 0; r < nf; ++r) cv[q * 5 + r] = 2.0 * sh.Xinv[q * nf + r];
+    }
+    for (int i = 0; i < 3; ++i) a.o_nu_out[(size_t)s * 3 + i] = sh.nu[i];
+    const double dof = (double)a.nbin * (double)m.nok - (double)(nf + m.nok);
+    const double chi2 = sh.Sd + st.fun;
+    a.o_chi2[s] = chi2;
+    a.o_red_chi2[s] = chi2 / dof;
+    a.o_snr[s] = sqrt(snr2);
+    a.o_nfev[s] = st.nfev;
+    a.o_status[s] = st.status;
+    if (a.o_init_used) for (int i = 0; i < 5; ++i) a.o_init_used[(size_t)s * 5 + i] = st.init[i];
+    if (a.o_fun) a.o_fun[s] = st.fun;
+  }
+}
+
+}  // namespace ppf

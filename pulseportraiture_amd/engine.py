@@ -1,0 +1,302 @@
+"""Device engine: owns a libppfit context and marshals arrays to the C ABI.
+
+torch is used only as plumbing: device allocations, H2D/D2H copies and the
+HIP stream handle.  All numerics run in the HIP kernels of libppfit.so.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+
+_NAN = float("nan")
+
+
+class PPFitError(RuntimeError):
+    pass
+
+
+def _dev_f64(x, dev, shape=None):
+    if x is None:
+        return None
+    if isinstance(x, torch.Tensor):
+        t = x.to(device=dev, dtype=torch.float64)
+    else:
+        t = torch.as_tensor(np.ascontiguousarray(x, dtype=np.float64), device=dev)
+    t = t.contiguous()
+    if shape is not None:
+        t = t.reshape(shape)
+    return t
+
+
+def _dev_i32(x, dev):
+    if x is None:
+        return None
+    if isinstance(x, torch.Tensor):
+        return x.to(device=dev, dtype=torch.int32).contiguous()
+    return torch.as_tensor(np.ascontiguousarray(x, dtype=np.int32), device=dev)
+
+
+def _dev_u8(x, dev):
+    if x is None:
+        return None
+    if isinstance(x, torch.Tensor):
+        return x.to(device=dev, dtype=torch.uint8).contiguous()
+    return torch.as_tensor(np.ascontiguousarray(x, dtype=np.uint8), device=dev)
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _nan_none(x):
+    """Array-like that may contain None (reference 'use the default') -> float64 with NaN."""
+    a = np.asarray(x, dtype=object)
+    return np.array([np.nan if v is None else float(v) for v in a.ravel()],
+                    dtype=np.float64).reshape(a.shape)
+
+
+def _bcast(x, n, width, dev, fill=_NAN):
+    """Per-subint row parameter: scalar, [width] or [n, width] -> [n, width] on dev."""
+    if x is None:
+        return torch.full((n, width), fill, dtype=torch.float64, device=dev)
+    if isinstance(x, torch.Tensor):
+        t = x.to(device=dev, dtype=torch.float64)
+    else:
+        t = torch.as_tensor(_nan_none(x), device=dev)
+    if t.numel() == n * width:
+        return t.reshape(n, width).contiguous()
+    if t.numel() in (1, width):
+        return t.reshape(1, -1).expand(n, width).contiguous()
+    raise PPFitError("cannot broadcast %s to (%d, %d)" % (tuple(t.shape), n, width))
+
+
+class Engine:
+    """One libppfit context on one HIP device (one per process/GPU)."""
+
+    def __init__(self, device=None, workspace_bytes=None):
+        if not torch.cuda.is_available():
+            raise PPFitError("no HIP device visible: libppfit has no CPU path")
+        self.lib = _lib.load_library()
+        if device is None:
+            device = torch.cuda.current_device()
+        self.device = torch.device("cuda", int(device))
+        ctx = ctypes.c_void_p()
+        rc = self.lib.ppf_ctx_create(int(device), ctypes.byref(ctx))
+        if rc != 0:
+            raise PPFitError("ppf_ctx_create failed (%d)" % rc)
+        self.ctx = ctx
+        if workspace_bytes is not None:
+            self._chk(self.lib.ppf_set_workspace_limit(self.ctx, int(workspace_bytes)))
+        self.bind_stream()
+
+    # -- plumbing ----------------------------------------------------------
+    def _chk(self, rc):
+        if rc != 0:
+            msg = self.lib.ppf_last_error(self.ctx)
+            raise PPFitError("libppfit error %d: %s" % (rc, msg.decode() if msg else ""))
+
+    def bind_stream(self, stream=None):
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        self.stream = s
+        self._chk(self.lib.ppf_set_stream(self.ctx, ctypes.c_void_p(s.cuda_stream)))
+
+    def synchronize(self):
+        self._chk(self.lib.ppf_synchronize(self.ctx))
+
+    def set_timing(self, on=True):
+        self._chk(self.lib.ppf_set_timing(self.ctx, int(bool(on))))
+
+    def kernel_time(self, name):
+        ms = ctypes.c_double()
+        n = ctypes.c_int64()
+        self._chk(self.lib.ppf_get_kernel_time(self.ctx, _lib.KERNEL_IDS[name],
+                                               ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+    def reset_kernel_times(self):
+        self._chk(self.lib.ppf_reset_kernel_times(self.ctx))
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.lib.ppf_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- batched fit -------------------------------------------------------
+    def fit_batch(self, data, model, freqs, P, init, fit_flags, nu_fit=None,
+                  nu_out=None, errs=None, chan_mask=None, weights=None,
+                  model_idx=None, log10_tau=False, option=0, is_toa=True,
+                  guess=False, guess_Ns=100, guess_wrap=True, guess_nu=None,
+                  guess_tau=None):
+        """fit_portrait_full over a batch (pptoaslib.py:928-1096).
+
+        data [nsub, nchan, nbin]; model [nmodel, nchan, nbin] (or [nchan, nbin]);
+        freqs [nsub, nchan] or [nchan]; P [nsub] or scalar; init [nsub, 5] or [5].
+        Returns a dict of device tensors.
+        """
+        dev = self.device
+        d = _dev_f64(data, dev)
+        if d.dim() == 2:
+            d = d.unsqueeze(0)
+        nsub, nchan, nbin = d.shape
+        m = _dev_f64(model, dev)
+        if m.dim() == 2:
+            m = m.unsqueeze(0)
+        if m.shape[1:] != (nchan, nbin):
+            raise PPFitError("model shape %s != (nmodel, %d, %d)" % (tuple(m.shape), nchan, nbin))
+        fr = _dev_f64(freqs, dev)
+        fr = fr.expand(nsub, nchan).contiguous() if fr.dim() == 1 else fr.reshape(nsub, nchan)
+        Pt = _dev_f64(P, dev).reshape(-1).expand(nsub).contiguous()
+        it = _bcast(init, nsub, 5, dev)
+        nf = _bcast(nu_fit, nsub, 3, dev)
+        no = _bcast(nu_out, nsub, 3, dev)
+        er = None if errs is None else _dev_f64(errs, dev).reshape(-1, nchan).expand(nsub, nchan).contiguous()
+        mk = None if chan_mask is None else _dev_u8(np.broadcast_to(np.asarray(chan_mask), (nsub, nchan)) if not isinstance(chan_mask, torch.Tensor) else chan_mask.expand(nsub, nchan), dev)
+        wt = None if weights is None else _dev_f64(weights, dev).reshape(-1, nchan).expand(nsub, nchan).contiguous()
+        mi = None if model_idx is None else _dev_i32(model_idx, dev)
+        gn = None if guess_nu is None else _bcast(guess_nu, nsub, 1, dev).reshape(nsub).contiguous()
+        gt = None if guess_tau is None else _bcast(guess_tau, nsub, 1, dev, 0.0).reshape(nsub).contiguous()
+        desc = _lib.FitDesc()
+        desc.nsub, desc.nchan, desc.nbin, desc.nmodel = nsub, nchan, nbin, m.shape[0]
+        for i in range(5):
+            desc.fit_flags[i] = int(bool(fit_flags[i]))
+        desc.log10_tau = int(bool(log10_tau))
+        desc.option = int(option)
+        desc.method = _lib.PPF_METHOD_TRUST_NCG
+        desc.is_toa = int(bool(is_toa))
+        desc.guess = int(bool(guess))
+        desc.guess_Ns = int(guess_Ns)
+        desc.guess_wrap = int(bool(guess_wrap))
+        keep = dict(d=d, m=m, fr=fr, P=Pt, it=it, nf=nf, no=no, er=er, mk=mk, wt=wt,
+                    mi=mi, gn=gn, gt=gt)
+        desc.data, desc.model, desc.model_idx = _ptr(d), _ptr(m), _ptr(mi)
+        desc.freqs, desc.errs, desc.chan_mask = _ptr(fr), _ptr(er), _ptr(mk)
+        desc.weights, desc.P, desc.init = _ptr(wt), _ptr(Pt), _ptr(it)
+        desc.nu_fit, desc.nu_out = _ptr(nf), _ptr(no)
+        desc.guess_nu, desc.guess_tau = _ptr(gn), _ptr(gt)
+        f64 = dict(dtype=torch.float64, device=dev)
+        out = dict(params=torch.empty(nsub, 5, **f64),
+                   param_errs=torch.empty(nsub, 5, **f64),
+                   nu_out=torch.empty(nsub, 3, **f64),
+                   cov=torch.empty(nsub, 5, 5, **f64),
+                   scales=torch.empty(nsub, nchan, **f64),
+                   scale_errs=torch.empty(nsub, nchan, **f64),
+                   channel_snrs=torch.empty(nsub, nchan, **f64),
+                   chi2=torch.empty(nsub, **f64), red_chi2=torch.empty(nsub, **f64),
+                   snr=torch.empty(nsub, **f64),
+                   nfev=torch.empty(nsub, dtype=torch.int32, device=dev),
+                   status=torch.empty(nsub, dtype=torch.int32, device=dev),
+                   init_used=torch.empty(nsub, 5, **f64),
+                   fun=torch.empty(nsub, **f64),
+                   cov_nosc=torch.empty(nsub, 5, 5, **f64))
+        res = _lib.FitResult()
+        for k in ["params", "param_errs", "nu_out", "cov", "scales", "scale_errs",
+                  "channel_snrs", "chi2", "red_chi2", "snr", "nfev", "status",
+                  "init_used", "fun", "cov_nosc"]:
+            setattr(res, k, _ptr(out[k]))
+        self._chk(self.lib.ppf_fit_portrait_batch(self.ctx, ctypes.byref(desc),
+                                                  ctypes.byref(res)))
+        out["_keep"] = keep  # inputs must outlive the stream-ordered call
+        return out
+
+    # -- other hot-path entry points ---------------------------------------
+    def phase_shift_batch(self, data, model, noise=None, Ns=100, bounds=(-0.5, 0.5),
+                          model_idx=None):
+        """fit_phase_shift over rows (pplib.py:2054-2100) -> [nprof, 6] device tensor."""
+        dev = self.device
+        d = _dev_f64(data, dev)
+        if d.dim() == 1:
+            d = d.unsqueeze(0)
+        nprof, nbin = d.shape
+        m = _dev_f64(model, dev)
+        if m.dim() == 1:
+            m = m.unsqueeze(0)
+        nz = None if noise is None else _bcast(noise, nprof, 1, dev).reshape(nprof).contiguous()
+        mi = None if model_idx is None else _dev_i32(model_idx, dev)
+        out = torch.empty(nprof, 6, dtype=torch.float64, device=dev)
+        self._chk(self.lib.ppf_phase_shift_batch(self.ctx, nprof, nbin, _ptr(d), _ptr(m),
+                                                 _ptr(mi), _ptr(nz), int(Ns),
+                                                 float(bounds[0]), float(bounds[1]),
+                                                 _ptr(out)))
+        out._keep = (d, m, nz, mi)
+        return out
+
+    def rotate_rows(self, rows, phase):
+        dev = self.device
+        r = _dev_f64(rows, dev)
+        shape = r.shape
+        r = r.reshape(-1, shape[-1])
+        ph = _dev_f64(phase, dev).reshape(-1).expand(r.shape[0]).contiguous()
+        out = torch.empty_like(r)
+        self._chk(self.lib.ppf_rotate_rows(self.ctx, r.shape[0], r.shape[1], _ptr(r),
+                                           _ptr(ph), _ptr(out)))
+        out._keep = (r, ph)
+        return out.reshape(shape)
+
+    def irfft_rows(self, spec, nbin):
+        dev = self.device
+        if isinstance(spec, torch.Tensor) and spec.is_complex():
+            sp = torch.view_as_real(spec.to(dev, torch.complex128).contiguous())
+        else:
+            sp = _dev_f64(np.stack([np.real(spec), np.imag(spec)], -1), dev)
+        rows = sp.reshape(-1, nbin // 2 + 1, 2)
+        out = torch.empty(rows.shape[0], nbin, dtype=torch.float64, device=dev)
+        self._chk(self.lib.ppf_irfft_rows(self.ctx, rows.shape[0], nbin, _ptr(rows), _ptr(out)))
+        out._keep = rows
+        return out
+
+    def noise_rows(self, rows):
+        dev = self.device
+        r = _dev_f64(rows, dev)
+        r2 = r.reshape(-1, r.shape[-1])
+        out = torch.empty(r2.shape[0], dtype=torch.float64, device=dev)
+        self._chk(self.lib.ppf_noise_rows(self.ctx, r2.shape[0], r2.shape[1], _ptr(r2), _ptr(out)))
+        out._keep = r2
+        return out.reshape(r.shape[:-1])
+
+    def rotate_accumulate(self, data, phase, weight, accum):
+        """accum [nchan, nharm, 2] (float64, device) += weighted rotated spectra."""
+        dev = self.device
+        d = _dev_f64(data, dev)
+        nsub, nchan, nbin = d.shape
+        ph = _dev_f64(phase, dev).reshape(nsub, nchan).contiguous()
+        w = _dev_f64(weight, dev).reshape(nsub, nchan).contiguous()
+        self._chk(self.lib.ppf_rotate_accumulate(self.ctx, nsub, nchan, nbin, _ptr(d), _ptr(ph),
+                                                 _ptr(w), _ptr(accum)))
+        return (d, ph, w)
+
+    def synth(self, model, phase, sigma, seed, sub0=0, out=None):
+        """Synthetic portraits [nsub, nchan, nbin] on device (pplib.py:3342-3377 math)."""
+        dev = self.device
+        m = _dev_f64(model, dev)
+        nchan, nbin = m.shape
+        ph = _dev_f64(phase, dev)
+        nsub = ph.numel() // nchan
+        ph = ph.reshape(nsub, nchan).contiguous()
+        if out is None:
+            out = torch.empty(nsub, nchan, nbin, dtype=torch.float64, device=dev)
+        self._chk(self.lib.ppf_synth_portraits(self.ctx, nsub, nchan, nbin, _ptr(m), _ptr(ph),
+                                               float(sigma), int(seed) & (2 ** 64 - 1),
+                                               int(sub0), _ptr(out)))
+        out._keep = (m, ph)
+        return out
+
+
+_engines = {}
+
+
+def get_engine(device=None):
+    """Process-wide engine per device."""
+    if device is None:
+        device = torch.cuda.current_device() if torch.cuda.is_available() else 0
+    key = int(device)
+    if key not in _engines:
+        _engines[key] = Engine(key)
+    return _engines[key]

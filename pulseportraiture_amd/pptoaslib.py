@@ -1,0 +1,149 @@
+"""pptoaslib drop-in: fit_portrait_full on the GPU (pptoaslib.py:928-1096).
+
+``fit_portrait_full`` keeps the reference signature and DataBunch keys; the
+FFTs, objective passes, trust-region solve, zero-covariance frequencies and
+the Woodbury covariance all run in libppfit (one workgroup per subint).
+``fit_portraits_batch`` is the batched form the drivers (get_TOAs, ppalign)
+use: one device call for many subints.
+"""
+import sys
+import time
+
+import numpy as np
+
+from .pplib import (DataBunch, Dconst, RCSTRINGS, scattering_times,
+                    scattering_portrait_FT)
+
+__all__ = ["fit_portrait_full", "fit_portraits_batch", "phase_shifts",
+           "phase_shifts_deriv", "rotate_portrait_full", "scattering_times",
+           "scattering_portrait_FT"]
+
+
+def phase_shifts(phi, DM, GM, freqs, nu_DM=np.inf, nu_GM=np.inf, P=None, mod=False):
+    """Per-channel delay [rot], pptoaslib.py:181-214."""
+    if P is None:
+        P, mod = 1.0, False
+    d = phi + Dconst * DM * (freqs ** -2 - nu_DM ** -2) / P + \
+        Dconst ** 2 * GM * (freqs ** -4 - nu_GM ** -4) / P
+    if mod:
+        d = np.where(abs(d) >= 0.5, d % 1, d)
+        d = np.where(d >= 0.5, d - 1.0, d)
+        if not np.shape(d):
+            d = np.float64(d)
+    return d
+
+
+def phase_shifts_deriv(freqs, nu_DM=np.inf, nu_GM=np.inf, P=None):
+    """pptoaslib.py:216-225."""
+    if P is None:
+        P = 1.0
+    dphi = np.ones(len(freqs)) if hasattr(freqs, "shape") else 1.0
+    return np.array([dphi, Dconst * (freqs ** -2 - nu_DM ** -2) / P,
+                     Dconst ** 2 * (freqs ** -4 - nu_GM ** -4) / P])
+
+
+def rotate_portrait_full(port, phi, DM, GM, freqs, nu_DM=np.inf, nu_GM=np.inf, P=None):
+    """Rotate/dedisperse a portrait on the GPU, pptoaslib.py:52-81."""
+    from .engine import get_engine
+    if P is None:
+        P = 1.0
+    ph = phase_shifts(phi, DM, GM, np.asarray(freqs, dtype=float), nu_DM, nu_GM, P)
+    return get_engine().rotate_rows(np.asarray(port, dtype=float), ph).cpu().numpy()
+
+
+def _nan(v):
+    return np.nan if v is None else float(v)
+
+
+def fit_portraits_batch(data, model, init, P, freqs, nu_fits=None, nu_outs=None,
+                        errs=None, fit_flags=(1, 1, 0, 0, 0), log10_tau=False, option=0,
+                        is_toa=True, chan_mask=None, weights=None, model_idx=None,
+                        guess=False, guess_Ns=100, guess_wrap=True, guess_nu=None,
+                        guess_tau=None, method="trust-ncg", device=None, to_host=True):
+    """Batched fit_portrait_full over subints; returns arrays keyed like its DataBunch."""
+    if method != "trust-ncg":
+        raise NotImplementedError(
+            "method %r: the device solver implements scipy 'trust-ncg' (the "
+            "reference default, pptoaslib.py:932)" % method)
+    from .engine import get_engine
+    eng = get_engine(device)
+    t0 = time.time()
+    out = eng.fit_batch(data, model, freqs, P, init, fit_flags, nu_fit=nu_fits,
+                        nu_out=nu_outs, errs=errs, chan_mask=chan_mask, weights=weights,
+                        model_idx=model_idx, log10_tau=log10_tau, option=option,
+                        is_toa=is_toa, guess=guess, guess_Ns=guess_Ns,
+                        guess_wrap=guess_wrap, guess_nu=guess_nu, guess_tau=guess_tau)
+    if not to_host:
+        return out
+    res = {k: v.cpu().numpy() for k, v in out.items() if not k.startswith("_")}
+    res["duration"] = np.full(len(res["chi2"]), (time.time() - t0) / len(res["chi2"]))
+    return res
+
+
+def _fit_batch_host(data, model, init, P, freqs, nu_fits, nu_outs, errs, fit_flags,
+                    log10_tau, legacy=False, **kw):
+    res = fit_portraits_batch(data, model, init, P, freqs,
+                              nu_fits=[_nan(v) for v in nu_fits],
+                              nu_outs=[_nan(v) for v in nu_outs], errs=errs,
+                              fit_flags=fit_flags, log10_tau=log10_tau, **kw)
+    if legacy:
+        cn = res["cov_nosc"]
+        S = (res["channel_snrs"] / res["scales"]) ** 2
+        res["legacy"] = dict(phase_err=cn[:, 0, 0] ** 0.5, DM_err=cn[:, 1, 1] ** 0.5,
+                             covariance=cn[:, 0, 1], scale_errs=S ** -0.5)
+    return res
+
+
+def result_bunch(res, i, fit_flags, duration=None):
+    """DataBunch of subint i in the layout of pptoaslib.py:1086-1095."""
+    ifit = np.where(fit_flags)[0]
+    nfit = len(ifit)
+    p = res["params"][i]
+    e = res["param_errs"][i]
+    cov = res["cov"][i][:nfit, :nfit]
+    return DataBunch(params=list(p), param_errs=e.copy(), phi=p[0], phi_err=e[0],
+                     DM=p[1], DM_err=e[1], GM=p[2], GM_err=e[2], tau=p[3],
+                     tau_err=e[3], alpha=p[4], alpha_err=e[4],
+                     scales=res["scales"][i], scale_errs=res["scale_errs"][i],
+                     nu_DM=res["nu_out"][i][0], nu_GM=res["nu_out"][i][1],
+                     nu_tau=res["nu_out"][i][2], covariance_matrix=cov,
+                     chi2=res["chi2"][i], red_chi2=res["red_chi2"][i], snr=res["snr"][i],
+                     channel_snrs=res["channel_snrs"][i],
+                     duration=res["duration"][i] if duration is None else duration,
+                     nfeval=int(res["nfev"][i]), return_code=int(res["status"][i]))
+
+
+def report_failure(status, sub_id=None, stream=sys.stderr):
+    """The reference's stderr note for a 'failed' fit, pptoaslib.py:1022-1033."""
+    success = status == 0
+    if success or status in (1, 2, 4):
+        return
+    rc = RCSTRINGS.get(str(status), "")
+    if sub_id is not None:
+        ii = sub_id[::-1].index("_")
+        stream.write("Fit 'failed' with return code %d: %s -- %s subint %s\n"
+                     % (status, rc, sub_id[:-ii - 1], sub_id[-ii:]))
+    else:
+        stream.write("Fit 'failed' with return code %d -- %s" % (status, rc))
+
+
+def fit_portrait_full(data_port, model_port, init_params, P, freqs,
+                      nu_fits=[None, None, None], nu_outs=[None, None, None], errs=None,
+                      fit_flags=[1, 1, 1, 1, 1],
+                      bounds=[(None, None), (None, None), (None, None), (None, None),
+                              (None, None)],
+                      log10_tau=True, option=0, sub_id=None, method="trust-ncg",
+                      is_toa=True, quiet=True):
+    """Fit phase, DM, GM, tau, alpha between data and model portraits (pptoaslib.py:928)."""
+    if method not in ("trust-ncg", "TNC", "Newton-CG"):
+        print("Method '%s' is not implemented." % method)
+        sys.exit()
+    data_port = np.asarray(data_port, dtype=float)
+    freqs = np.asarray(freqs, dtype=float)
+    res = _fit_batch_host(data_port[None], np.asarray(model_port, dtype=float)[None],
+                          list(init_params), P, freqs, nu_fits, nu_outs,
+                          None if errs is None else np.asarray(errs, dtype=float),
+                          fit_flags, log10_tau, option=option, is_toa=is_toa,
+                          method=method)
+    report_failure(int(res["status"][0]), sub_id)
+    return result_bunch(res, 0, fit_flags)

@@ -1,0 +1,42 @@
+"""The C-ABI library builds, loads and exports every symbol of include/ppfit.h."""
+import os
+import re
+
+from tests.conftest import ROOT
+
+
+def header_symbols():
+    txt = open(os.path.join(ROOT, "include", "ppfit.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(ppf_\w+)\s*\(", txt, re.M)))
+
+
+def test_header_declares_entry_points():
+    syms = header_symbols()
+    for s in ["ppf_ctx_create", "ppf_fit_portrait_batch", "ppf_phase_shift_batch",
+              "ppf_rotate_rows", "ppf_rotate_accumulate", "ppf_irfft_rows",
+              "ppf_noise_rows", "ppf_synth_portraits"]:
+        assert s in syms
+
+
+def test_library_exports_all_header_symbols():
+    from pulseportraiture_amd import build, _lib
+    build.build()
+    lib = _lib.load_library()
+    for s in header_symbols():
+        assert hasattr(lib, s), s
+    assert lib.ppf_version() == 1
+
+
+def test_binding_covers_header():
+    from pulseportraiture_amd import _lib
+    assert set(header_symbols()) == set(_lib.EXPORTS)
+
+
+def test_no_device_fails_loudly():
+    import torch
+    import pytest
+    if torch.cuda.is_available():
+        pytest.skip("device present")
+    from pulseportraiture_amd.engine import Engine, PPFitError
+    with pytest.raises(PPFitError):
+        Engine(0)
