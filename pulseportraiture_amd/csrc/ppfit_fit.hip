@@ -555,7 +555,7 @@ struct SolveShared {
   double x[5], xp[5];
   double out[48];
   double red[kWaves][48];
-  int done, nok;
+  int done, nok, slot;  // slot: accumulator half holding the accepted point
 };
 
 template <bool SCAT>
@@ -571,13 +571,13 @@ __global__ __launch_bounds__(kBlock) void k_solve(FitArgs a) {
   const double P = a.P[s];
   if (tid < 5) sh.x[tid] = st.x[tid];
   if (tid < 3) refs[tid] = st.refs[tid];
-  if (tid == 0) sh.done = (m.nok == 0);
+  if (tid == 0) { sh.done = (m.nok == 0); sh.slot = 0; }
   __syncthreads();
   double* acc0 = a.acc + (size_t)c * 2 * a.nchan * NACC;
   // wave-0 solver state (lane i < 5 owns component i; scalars are uniform)
   double f = 0.0, g = 0.0, xl = 0.0, Hrow[5] = {0, 0, 0, 0, 0};
   double tr = 1.0, predv = 0.0, pl = 0.0;
-  int hits = 0, k = 0, status = (m.nok == 0) ? -1 : 0, nfev = 0, slot = 0;
+  int hits = 0, k = 0, status = (m.nok == 0) ? -1 : 0, nfev = 0;
   auto load_fgh = [&](double& ff, double& gg, double (&HH)[5]) {
     ff = sh.out[0];
     gg = lane < 5 ? sh.out[1 + lane] : 0.0;
@@ -610,7 +610,8 @@ __global__ __launch_bounds__(kBlock) void k_solve(FitArgs a) {
     }
     __syncthreads();
     if (sh.done) break;
-    double* sl = acc0 + (size_t)(slot ^ 1) * a.nchan * NACC;
+    // every wave writes the proposal into the half the accepted point is not in
+    double* sl = acc0 + (size_t)(sh.slot ^ 1) * a.nchan * NACC;
     sweep<0, SCAT>(a, m, c, s, sh.xp, refs, P, sl, sh.out, sh.red);
     if (tid < 64) {
       double fp, gp, Hp[5] = {0, 0, 0, 0, 0};
@@ -631,7 +632,7 @@ __global__ __launch_bounds__(kBlock) void k_solve(FitArgs a) {
           g = gp;
 #pragma unroll
           for (int j = 0; j < 5; ++j) Hrow[j] = Hp[j];
-          slot ^= 1;
+          if (lane == 0) sh.slot ^= 1;
           if (lane < 5) sh.x[lane] = xl;
         }
         k += 1;
@@ -648,7 +649,7 @@ __global__ __launch_bounds__(kBlock) void k_solve(FitArgs a) {
     st.fun = m.nok ? f : NAN;
     st.nfev = m.nok ? nfev : 0;
     st.status = status;
-    st.slot = slot;
+    st.slot = sh.slot;
     const double tl = a.log10_tau ? pow(10.0, sh.x[3]) : sh.x[3];
     st.scat_post = SCAT && tl != 0.0;
   }

@@ -1,0 +1,244 @@
+"""ppalign drop-in: iterative align-and-average (ppalign.py:54-243) on the GPU.
+
+Per iteration every (archive, subint) unit is fitted in one batched device
+call (phase guess with Ns = nbin at nu_fit, then phase[+DM] trust-ncg), then
+rotated and accumulated with weights scales/errs^2 in the Fourier domain
+(ppf_rotate_accumulate; linear, so equal to summing irfft'd rotations).  With
+torch.distributed initialised, units are sharded contiguously over ranks and
+the only collective is one all-reduce (sum, fp64) of the [nchan, nbin/2+1]
+spectrum and the channel weights per iteration -- RCCL over xGMI with the
+"nccl" backend.  Every rank then divides locally and holds the new template.
+"""
+import numpy as np
+import torch
+
+from . import archive as _arch
+from .pplib import (DataBunch, Dconst, guess_fit_freq, gaussian_profile, rotate_data,
+                    fit_phase_shift)
+from .pptoaslib import fit_portraits_batch
+
+rm_baseline = False
+
+
+def shard_range(n, rank, world):
+    """Contiguous [lo, hi) slice of n units for rank (sizes differ by <= 1)."""
+    base, extra = divmod(n, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+def dist_info():
+    if torch.distributed.is_available() and torch.distributed.is_initialized():
+        return torch.distributed.get_rank(), torch.distributed.get_world_size()
+    return 0, 1
+
+
+def allreduce_sum(*tensors):
+    """Sum tensors over all ranks in place (one fused buffer, one collective)."""
+    rank, world = dist_info()
+    if world == 1:
+        return tensors
+    flat = torch.cat([t.reshape(-1) for t in tensors])
+    torch.distributed.all_reduce(flat, op=torch.distributed.ReduceOp.SUM)
+    off = 0
+    for t in tensors:
+        n = t.numel()
+        t.copy_(flat[off:off + n].reshape(t.shape))
+        off += n
+    return tensors
+
+
+def _units(datafiles, model_data, SNR_cutoff, quiet, skip_these, state=None):
+    """Load archives and list (archive, subint, ichans, model_ichans) units."""
+    units, archives = [], {}
+    for name in datafiles:
+        try:
+            data = _arch.load_data(name)
+        except RuntimeError:
+            if not quiet:
+                print("%s: cannot load_data().  Skipping it." % name)
+            skip_these.append(name)
+            continue
+        if data.nbin != model_data.nbin:
+            if not quiet:
+                print("%s: %d != %d phase bins.  Skipping it." % (name, data.nbin,
+                                                                 model_data.nbin))
+            skip_these.append(name)
+            continue
+        if data.prof_SNR < SNR_cutoff:
+            skip_these.append(name)
+            continue
+        try:
+            fd = data.freqs - model_data.freqs
+            same = fd.min() == fd.max() == 0.0
+        except ValueError:
+            same = False
+        archives[name] = data
+        for isub in data.ok_isubs:
+            if same:
+                ichans = np.intersect1d(data.ok_ichans[isub], model_data.ok_ichans[0])
+                mich = ichans
+            else:
+                ichans = np.asarray(data.ok_ichans[isub])
+                mich = np.array([np.argmin(abs(model_data.freqs[0] - data.freqs[isub, c]))
+                                 for c in ichans])
+            units.append((name, int(isub), ichans, mich))
+    return units, archives
+
+
+def align_archives(metafile, initial_guess, fit_dm=True, tscrunch=False, pscrunch=True,
+                   SNR_cutoff=0.0, outfile=None, norm=None, rot_phase=0.0, place=None,
+                   niter=1, quiet=False, return_weights=False):
+    """Iteratively align and average archives; returns aligned_port[npol, nchan, nbin].
+
+    The reference writes the result into a PSRCHIVE archive; here the portrait
+    is returned (and written with archive.save_archive when ``outfile`` ends in
+    .npz).
+    """
+    from .engine import get_engine
+    if tscrunch:
+        raise NotImplementedError("tscrunch needs PSRCHIVE (out of scope)")
+    if isinstance(metafile, str) and _arch.file_is_type(metafile, "ASCII"):
+        datafiles = [ln.strip() for ln in open(metafile).readlines() if ln.strip()]
+        if outfile is None:
+            outfile = metafile + ".algnd.fits"
+    else:
+        datafiles = list(metafile) if not isinstance(metafile, str) else [metafile]
+    model_data = _arch.load_data(initial_guess)
+    npol = 1 if pscrunch else model_data.npol
+    model_port = np.asarray((model_data.masks * model_data.subints)[0, 0], dtype=np.float64)
+    nchan, nbin = model_port.shape
+    nharm = nbin // 2 + 1
+    eng = get_engine()
+    dev = eng.device
+    rank, world = dist_info()
+    skip_these = []
+    units, archives = _units(datafiles, model_data, SNR_cutoff, quiet, skip_these)
+    lo, hi = shard_range(len(units), rank, world)
+    mine = units[lo:hi]
+    count = 1
+    aligned = None
+    tw = None
+    while niter:
+        if not quiet and rank == 0:
+            print("Doing iteration %d..." % count)
+        accum = torch.zeros(npol, nchan, nharm, 2, dtype=torch.float64, device=dev)
+        tw = torch.zeros(nchan, dtype=torch.float64, device=dev)
+        multi = [u for u in mine if len(u[2]) > 1]
+        single = [u for u in mine if len(u[2]) <= 1]
+        if multi:
+            _fit_and_accumulate(eng, multi, archives, model_port, model_data.freqs[0],
+                                fit_dm, npol, accum, tw)
+        for u in single:  # 1-channel hack, ppalign.py:196-201
+            _single_channel(u, archives, model_port, npol, accum, tw, dev)
+        allreduce_sum(accum, tw)
+        spec = torch.view_as_complex(accum).reshape(npol * nchan, nharm)
+        port = eng.irfft_rows(spec, nbin).reshape(npol, nchan, nbin)
+        good = tw > 0
+        port[:, good] = port[:, good] / tw[good][None, :, None]
+        aligned = port.cpu().numpy()
+        model_port = aligned[0]
+        niter -= 1
+        count += 1
+    if norm in ("mean", "max", "prof", "rms", "abs"):
+        from .pplib import get_noise
+        for ipol in range(npol):
+            aligned[ipol] = _normalize(aligned[ipol], norm, get_noise)
+    if rot_phase:
+        aligned = rotate_data(aligned, rot_phase)
+    if place is not None:
+        prof = np.average(aligned[0], axis=0)
+        delta = prof.max() * gaussian_profile(len(prof), place, 0.0001)
+        aligned = rotate_data(aligned, fit_phase_shift(prof, delta, Ns=nbin).phase)
+    if outfile is not None and str(outfile).endswith(".npz") and rank == 0:
+        w = np.where(tw.cpu().numpy() > 0, 1.0, 0.0)
+        _arch.save_archive(outfile, dict(subints=aligned[None], freqs=model_data.freqs[0],
+                                         Ps=model_data.Ps[:1], epochs=model_data.epochs[:1],
+                                         weights=w[None], DM=0.0))
+    if return_weights:
+        return aligned, tw.cpu().numpy()
+    return aligned
+
+
+def _fit_and_accumulate(eng, units, archives, model_port, model_freqs, fit_dm, npol,
+                        accum, tw):
+    nchan, nbin = model_port.shape
+    n = len(units)
+    data = np.zeros((n, nchan, nbin))
+    freqs = np.zeros((n, nchan))
+    errs = np.ones((n, nchan))
+    mask = np.zeros((n, nchan), dtype=np.uint8)
+    wts = np.zeros((n, nchan))
+    P = np.zeros(n)
+    DMg = np.zeros(n)
+    nu_fit = np.zeros(n)
+    for i, (name, isub, ichans, mich) in enumerate(units):
+        d = archives[name]
+        # unit channel c sits in template slot mich[c]; other slots are masked
+        data[i, mich] = d.subints[isub, 0, ichans]
+        freqs[i] = model_freqs
+        freqs[i, mich] = d.freqs[isub, ichans]
+        noise = d.noise_stds[isub, 0, ichans] if d.get("noise_stds") is not None else \
+            eng.noise_rows(d.subints[isub, 0, ichans]).cpu().numpy()
+        errs[i, mich] = noise
+        mask[i, mich] = 1
+        wts[i, mich] = d.weights[isub, ichans]
+        P[i] = d.Ps[isub]
+        DMg[i] = d.DM
+        nu_fit[i] = guess_fit_freq(d.freqs[isub, ichans], d.SNRs[isub, 0, ichans])
+    init = np.stack([np.zeros(n), DMg, np.zeros(n), np.zeros(n), np.zeros(n)], 1)
+    flags = [1, int(bool(fit_dm)), 0, 0, 0]
+    res = fit_portraits_batch(data, model_port, init, P, freqs,
+                              nu_fits=np.stack([nu_fit] * 3, 1), errs=errs, fit_flags=flags,
+                              log10_tau=False, chan_mask=mask, weights=wts, guess=True,
+                              guess_Ns=nbin, guess_wrap=False, guess_nu=nu_fit)
+    phase = res["params"][:, 0]
+    DM = res["params"][:, 1]
+    nu_ref = res["nu_out"][:, 0]
+    # rotate_data(port, phase, DM, P, freqs, nu_ref) per channel (pplib.py:2406-2415)
+    ph = phase[:, None] + (Dconst * DM / P)[:, None] * (freqs ** -2.0 - nu_ref[:, None] ** -2.0)
+    w = np.where(mask > 0, res["scales"] / errs ** 2, 0.0)
+    for ipol in range(npol):
+        pol = np.zeros((n, nchan, nbin))
+        for i, (name, isub, ichans, mich) in enumerate(units):
+            pol[i, mich] = archives[name].subints[isub, ipol, ichans]
+        eng.rotate_accumulate(pol, ph, w, accum[ipol])
+    tw += torch.as_tensor(w.sum(axis=0), device=tw.device)
+    return res
+
+
+def _single_channel(u, archives, model_port, npol, accum, tw, dev):
+    name, isub, ichans, mich = u
+    d = archives[name]
+    nbin = model_port.shape[1]
+    errs = d.noise_stds[isub, 0, ichans] if d.get("noise_stds") is not None else [None]
+    r = fit_phase_shift(d.subints[isub, 0, ichans][0], model_port[mich][0], errs[0], Ns=nbin)
+    from .engine import get_engine
+    eng = get_engine()
+    w = np.array([[r.scale / errs[0] ** 2]]) if errs[0] is not None else np.array([[r.scale]])
+    for ipol in range(npol):
+        acc = torch.zeros_like(accum[ipol])
+        eng.rotate_accumulate(d.subints[isub, ipol, ichans][None], np.array([[r.phase]]), w, acc)
+        accum[ipol][int(mich[0])] += acc[0]
+    tw[int(mich[0])] += float(w[0, 0])
+
+
+def _normalize(port, method, get_noise):
+    """normalize_portrait for the final template (pplib.py:2462-2507)."""
+    out = np.zeros(port.shape)
+    for i in range(len(port)):
+        if not port[i].any():
+            continue
+        if method == "mean":
+            nrm = port[i].mean()
+        elif method == "max":
+            nrm = port[i].max()
+        elif method == "rms":
+            nrm = get_noise(port[i])
+        elif method == "abs":
+            nrm = (port[i] ** 2).sum() ** 0.5
+        else:
+            good = np.where(port.sum(axis=1) != 0.0)[0]
+            nrm = fit_phase_shift(port[i], np.average(port[good], axis=0)).scale
+        out[i] = port[i] / nrm
+    return out
