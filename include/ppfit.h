@@ -55,14 +55,16 @@ extern "C" {
 /* kernel ids for ppf_get_kernel_time */
 #define PPF_K_MODEL_FFT 0
 #define PPF_K_DATA_XSPEC 1
-#define PPF_K_FIT 2
+#define PPF_K_SOLVE 2
 #define PPF_K_PHASE_SHIFT 3
 #define PPF_K_ROTATE 4
 #define PPF_K_ROT_ACCUM 5
 #define PPF_K_SYNTH 6
 #define PPF_K_IRFFT 7
 #define PPF_K_NOISE 8
-#define PPF_NUM_KERNELS 9
+#define PPF_K_GUESS 9
+#define PPF_K_POST 10
+#define PPF_NUM_KERNELS 11
 
 typedef struct ppf_ctx ppf_ctx;
 

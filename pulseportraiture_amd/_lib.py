@@ -12,8 +12,9 @@ LIB_PATH = os.path.join(HERE, "libppfit.so")
 
 PPF_OK = 0
 PPF_METHOD_TRUST_NCG = 0
-KERNEL_IDS = {"model_fft": 0, "data_xspec": 1, "fit": 2, "phase_shift": 3,
-              "rotate": 4, "rot_accum": 5, "synth": 6, "irfft": 7, "noise": 8}
+KERNEL_IDS = {"model_fft": 0, "data_xspec": 1, "solve": 2, "phase_shift": 3,
+              "rotate": 4, "rot_accum": 5, "synth": 6, "irfft": 7, "noise": 8,
+              "guess": 9, "post": 10}
 
 _dp = ctypes.c_void_p  # device pointers travel as plain addresses
 

@@ -393,18 +393,18 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
                                                ctx->stream, sa));
         }))
       return r;
-    if (int r = timed(ctx, PPF_K_FIT, [&] {
+    if (int r = timed(ctx, PPF_K_GUESS, [&] {
           hipLaunchKernelGGL(k_guess, dim3(nc), dim3(kBlock), d->guess ? lds_guess : 0,
                              ctx->stream, fa);
         }))
       return r;
     // each subint runs in exactly one of the phase-only / scattering variants
-    if (int r = timed(ctx, PPF_K_FIT, [&] {
+    if (int r = timed(ctx, PPF_K_SOLVE, [&] {
           hipLaunchKernelGGL(k_solve<false>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
           hipLaunchKernelGGL(k_solve<true>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
         }))
       return r;
-    if (int r = timed(ctx, PPF_K_FIT, [&] {
+    if (int r = timed(ctx, PPF_K_POST, [&] {
           hipLaunchKernelGGL(k_post<false>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
           hipLaunchKernelGGL(k_post<true>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
         }))
