@@ -40,6 +40,22 @@ CONFIGS = {
 }
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+# HBM bytes per subint per kernel from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
+# passes over this same bench (tools/profile_r1.sh + tools/pmc_summary.py).
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+KERNEL_SYMBOL = {"solve": "k_solve<false>", "data_xspec": "k_data_xspec<10>",
+                 "post": "k_post<false>", "guess": "k_guess"}
+
+
+def pmc_traffic(kernel, nsub, nbin, nchan, config):
+    """Counter-measured HBM bytes per launch for the headline config, else None."""
+    if config != "headline" or nbin != 2048 or nchan != 64 or not os.path.exists(PMC_TRAFFIC):
+        return None
+    rec = json.load(open(PMC_TRAFFIC))
+    k = rec["kernels"].get(KERNEL_SYMBOL.get(kernel, ""))
+    if k is None:
+        return None
+    return k["bytes_per_subint"] * nsub
 
 
 def parse():
@@ -50,7 +66,7 @@ def parse():
     ap.add_argument("--config", default="headline", choices=sorted(CONFIGS))
     ap.add_argument("--nsub", type=int, default=None, help="subints per GPU (override)")
     ap.add_argument("--seed", type=int, default=20240917)
-    ap.add_argument("--cpu-sample", type=int, default=60,
+    ap.add_argument("--cpu-sample", type=int, default=300,
                     help="subints the CPU oracle fits for the baseline (0: skip)")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP events")
     return ap.parse_args()
@@ -164,9 +180,12 @@ def main():
             bytes_launch = nsub * nharm * 16.0 * 2
             what = "k_guess: R and mean-template spectra"
         achieved = bytes_launch / avg_s / 1e9
+        traffic = pmc_traffic(dom, nsub, nbin, nchan, args.config)
         roof = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": None, "avg_launch_ms": round(ms / max(n, 1), 4),
+                "traffic": traffic, "traffic_unit": "bytes/launch",
+                "traffic_source": os.path.relpath(PMC_TRAFFIC, ROOT) if traffic else None,
+                "avg_launch_ms": round(ms / max(n, 1), 4),
                 "algorithmic_bytes_per_launch": bytes_launch, "bytes_model": what,
                 "kernel_ms_per_step": {k: round(v[0] / max(v[1], 1), 4) for k, v in ktimes.items()}}
 
