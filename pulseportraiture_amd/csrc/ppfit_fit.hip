@@ -124,22 +124,42 @@ __device__ __forceinline__ void block_sum_vec(double (&v)[N], double (*red)[48])
 // ---------------------------------------------------------------------------
 // Cell sweeps over one channel row of X (lane's harmonics k = h + 8 j)
 // ---------------------------------------------------------------------------
+// The row is streamed with the next U harmonics' loads in flight while the
+// current U are accumulated (software pipelining: one HBM latency per row,
+// not one per step); the accumulation order is unchanged.
+constexpr int kPipe = 4;  // divides the 32-step re-seed period
+
 __device__ __forceinline__ void cells_phase(const double2* __restrict__ Xr, int J, int h,
                                             double phif, double* acc) {
   const double2 step = turn_phasor(8.0, phif);
+  const double2 zero = cmk(0.0, 0.0);
   double2 e = cmk(1.0, 0.0);
   double a0 = 0.0, a1 = 0.0, a2 = 0.0;
-  for (int j = 0; j < J; ++j) {
-    const int k = h + 8 * j;
-    if ((j & 31) == 0) e = turn_phasor((double)k, phif);
-    else e = cmul(e, step);
-    const double2 x = Xr[k];
-    const double wr = fma(x.x, e.x, -x.y * e.y);
-    const double wi = fma(x.x, e.y, x.y * e.x);
-    const double kd = (double)k;
-    a0 += wr;
-    a1 = fma(kd, wi, a1);
-    a2 = fma(kd * kd, wr, a2);
+  double2 nx[kPipe];
+#pragma unroll
+  for (int u = 0; u < kPipe; ++u) nx[u] = u < J ? Xr[h + 8 * u] : zero;
+  for (int j0 = 0; j0 < J; j0 += kPipe) {
+    double2 cx[kPipe];
+#pragma unroll
+    for (int u = 0; u < kPipe; ++u) cx[u] = nx[u];
+#pragma unroll
+    for (int u = 0; u < kPipe; ++u) {
+      const int j = j0 + kPipe + u;
+      nx[u] = j < J ? Xr[h + 8 * j] : zero;
+    }
+#pragma unroll
+    for (int u = 0; u < kPipe; ++u) {
+      const int k = h + 8 * (j0 + u);
+      if (u == 0 && (j0 & 31) == 0) e = turn_phasor((double)k, phif);
+      else e = cmul(e, step);
+      const double2 x = cx[u];
+      const double wr = fma(x.x, e.x, -x.y * e.y);
+      const double wi = fma(x.x, e.y, x.y * e.x);
+      const double kd = (double)k;
+      a0 += wr;
+      a1 = fma(kd, wi, a1);
+      a2 = fma(kd * kd, wr, a2);
+    }
   }
   acc[0] = a0; acc[1] = a1; acc[2] = a2;
   for (int i = 3; i < NACC; ++i) acc[i] = 0.0;
@@ -151,40 +171,59 @@ __device__ __forceinline__ void cells_phase(const double2* __restrict__ Xr, int 
 __device__ __forceinline__ void cells_scat(const double2* __restrict__ Xr,
                                            const double2* __restrict__ Mr, int J, int h,
                                            double phif, double taun, double* acc) {
+  constexpr int U = 2;
   const double2 step = turn_phasor(8.0, phif);
   const double itau = 1.0 / taun;
   const double w0 = kTwoPi * taun;
+  const double2 zero = cmk(0.0, 0.0);
   double2 e = cmk(1.0, 0.0);
   double a[NACC];
   for (int i = 0; i < NACC; ++i) a[i] = 0.0;
-  for (int j = 0; j < J; ++j) {
-    const int k = h + 8 * j;
-    if ((j & 31) == 0) e = turn_phasor((double)k, phif);
-    else e = cmul(e, step);
-    const double2 x = Xr[k];
-    const double2 mm = Mr[k];
-    const double m2 = cabs2(mm);
-    const double2 W = cmul(x, e);
-    const double kd = (double)k;
-    const double aa = w0 * kd;
-    const double id = 1.0 / fma(aa, aa, 1.0);
-    const double2 B = cmk(id, -aa * id);
-    const double2 Bm1 = cmk(B.x - 1.0, B.y);
-    const double2 f = cscale(cmul(B, Bm1), itau);
-    const double2 g1 = cscale(cmul(f, Bm1), 2.0 * itau);
-    const double2 WB = cmulc(W, B);
-    const double2 Wf = cmulc(W, f);
-    const double2 Wg = cmulc(W, g1);
-    a[0] += WB.x;
-    a[1] = fma(kd, WB.y, a[1]);
-    a[2] = fma(kd * kd, WB.x, a[2]);
-    a[3] += Wf.x;
-    a[4] = fma(kd, Wf.y, a[4]);
-    a[5] += Wg.x;
-    a[6] = fma(cabs2(B), m2, a[6]);
-    a[7] = fma(fma(B.x, f.x, B.y * f.y), m2, a[7]);
-    a[8] = fma(cabs2(f), m2, a[8]);
-    a[9] = fma(fma(B.x, g1.x, B.y * g1.y), m2, a[9]);
+  double2 nx[U], nm[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    nx[u] = u < J ? Xr[h + 8 * u] : zero;
+    nm[u] = u < J ? Mr[h + 8 * u] : zero;
+  }
+  for (int j0 = 0; j0 < J; j0 += U) {
+    double2 cx[U], cm[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) { cx[u] = nx[u]; cm[u] = nm[u]; }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = j0 + U + u;
+      nx[u] = j < J ? Xr[h + 8 * j] : zero;
+      nm[u] = j < J ? Mr[h + 8 * j] : zero;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = h + 8 * (j0 + u);
+      if (u == 0 && (j0 & 31) == 0) e = turn_phasor((double)k, phif);
+      else e = cmul(e, step);
+      const double2 x = cx[u];
+      const double m2 = cabs2(cm[u]);
+      const double2 W = cmul(x, e);
+      const double kd = (double)k;
+      const double aa = w0 * kd;
+      const double id = 1.0 / fma(aa, aa, 1.0);
+      const double2 B = cmk(id, -aa * id);
+      const double2 Bm1 = cmk(B.x - 1.0, B.y);
+      const double2 f = cscale(cmul(B, Bm1), itau);
+      const double2 g1 = cscale(cmul(f, Bm1), 2.0 * itau);
+      const double2 WB = cmulc(W, B);
+      const double2 Wf = cmulc(W, f);
+      const double2 Wg = cmulc(W, g1);
+      a[0] += WB.x;
+      a[1] = fma(kd, WB.y, a[1]);
+      a[2] = fma(kd * kd, WB.x, a[2]);
+      a[3] += Wf.x;
+      a[4] = fma(kd, Wf.y, a[4]);
+      a[5] += Wg.x;
+      a[6] = fma(cabs2(B), m2, a[6]);
+      a[7] = fma(fma(B.x, f.x, B.y * f.y), m2, a[7]);
+      a[8] = fma(cabs2(f), m2, a[8]);
+      a[9] = fma(fma(B.x, g1.x, B.y * g1.y), m2, a[9]);
+    }
   }
   for (int i = 0; i < NACC; ++i) acc[i] = a[i];
 }
