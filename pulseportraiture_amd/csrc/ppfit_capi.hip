@@ -389,7 +389,7 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
     sa.sub0 = (int)s0;
     fa.sub0 = (int)s0;
     if (int r = timed(ctx, PPF_K_DATA_XSPEC, [&] {
-          LOGN_SWITCH(logN, hipLaunchKernelGGL(k_data_xspec<LG>, dim3(nc), dim3(kBlock), 0,
+          LOGN_SWITCH(logN, hipLaunchKernelGGL(k_data_xspec<LG>, dim3(nc), dim3(kBlock), (size_t)nchan * sizeof(double2),
                                                ctx->stream, sa));
         }))
       return r;

@@ -6,8 +6,21 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 namespace ppf {
+
+// Compile-time loop: f(std::integral_constant<int, i>) for i in [0, N), so
+// register arrays indexed by i stay in registers.
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for_impl(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for_impl<I + 1, N>(f);
+  }
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) { static_for_impl<0, N>(f); }
 
 // pplib.py:48-51: Dconst = 0.000241**-1 (bit-identical double)
 constexpr double kDconst = 0x1.03560a9f560aap+12;
@@ -184,6 +197,79 @@ __device__ void lds_fft(double2* buf, const double2* __restrict__ tw) {
     __syncthreads();
     Ns *= 4;
   }
+}
+
+// Forward FFT like lds_fft<LOGN, false>, with its twiddles read from an LDS
+// table twl[e] = e^{-2 pi i e / N}, e < 3N/4 (filled once per workgroup):
+// radix-4 pass with span Ns needs exponents r k N / (4 Ns) < 3N/4.
+template <int LOGN>
+__device__ __forceinline__ void lds_fft_twl(double2* buf, const double2* twl) {
+  constexpr int N = 1 << LOGN;
+  constexpr int Q = N / 4;
+  constexpr int B4 = (Q + kBlock - 1) / kBlock;
+  const int tid = threadIdx.x;
+  int Ns = 1;
+  if constexpr (LOGN & 1) {
+    constexpr int H = N / 2;
+    constexpr int B2 = (H + kBlock - 1) / kBlock;
+    double2 a[B2], b[B2];
+#pragma unroll
+    for (int c = 0; c < B2; ++c) {
+      const int j = tid + c * kBlock;
+      if (j < H) { a[c] = buf[j]; b[c] = buf[j + H]; }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < B2; ++c) {
+      const int j = tid + c * kBlock;
+      if (j < H) { buf[2 * j] = cadd(a[c], b[c]); buf[2 * j + 1] = csub(a[c], b[c]); }
+    }
+    __syncthreads();
+    Ns = 2;
+  }
+#pragma unroll
+  for (int p = 0; p < LOGN / 2; ++p) {
+    double2 v[B4][4];
+#pragma unroll
+    for (int c = 0; c < B4; ++c) {
+      const int j = tid + c * kBlock;
+      if (j < Q) {
+        const int k = j & (Ns - 1);
+        const int e = k * (N / (4 * Ns));
+        v[c][0] = buf[j];
+#pragma unroll
+        for (int r = 1; r < 4; ++r) v[c][r] = cmul(buf[j + r * Q], twl[r * e]);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < B4; ++c) {
+      const int j = tid + c * kBlock;
+      if (j < Q) {
+        radix4<false>(v[c][0], v[c][1], v[c][2], v[c][3]);
+        const int k = j & (Ns - 1);
+        const int d = (j - k) * 4 + k;
+        buf[d] = v[c][0];
+        buf[d + Ns] = v[c][1];
+        buf[d + 2 * Ns] = v[c][2];
+        buf[d + 3 * Ns] = v[c][3];
+      }
+    }
+    __syncthreads();
+    Ns *= 4;
+  }
+}
+
+// rfft_post with the twiddle e^{-2 pi i k / 2N} passed in (a register).
+template <int LOGN>
+__device__ __forceinline__ double2 rfft_post_w(const double2* buf, int k, double2 w) {
+  constexpr int N = 1 << LOGN;
+  const double2 zk = buf[k & (N - 1)];
+  const double2 zc = cconj(buf[(N - k) & (N - 1)]);
+  const double2 e = cscale(cadd(zk, zc), 0.5);
+  const double2 dd = csub(zk, zc);
+  const double2 o = cmk(0.5 * dd.y, -0.5 * dd.x);
+  return cadd(e, cmul(w, o));
 }
 
 // Real-input spectrum X_k (k in [0, N]) of the 2N-point real row packed as

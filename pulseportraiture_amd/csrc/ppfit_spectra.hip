@@ -71,14 +71,53 @@ __global__ __launch_bounds__(kBlock) void k_model_spec(const double* __restrict_
 //   R[c][k]    += w_n D_nk e^{2 pi i k phi_n},  phi_n = Dconst DM (nu_n^-2 -
 //                 nu_g^-2) / P  (rotate_data with DM, pplib.py:2406-2415)
 // ---------------------------------------------------------------------------
+// Row prefetch into registers, kept as plain doubles (a double2 array
+// carried across the channel loop is copied with memcpy and lands in scratch).
+template <int LOGN>
+struct RowRegs {
+  static constexpr int N = 1 << LOGN;
+  static constexpr int LI = N >= kBlock ? N / kBlock : 1;
+  double x[LI], y[LI];
+  __device__ __forceinline__ void load(const double* __restrict__ src) {
+    const double2* r2 = reinterpret_cast<const double2*>(src);
+#pragma unroll
+    for (int i = 0; i < LI; ++i) {
+      const int j = threadIdx.x + i * kBlock;
+      if (N >= kBlock || j < N) {
+        const double2 v = r2[j];
+        x[i] = v.x;
+        y[i] = v.y;
+      }
+    }
+  }
+  __device__ __forceinline__ void store(double2* buf) const {
+#pragma unroll
+    for (int i = 0; i < LI; ++i) {
+      const int j = threadIdx.x + i * kBlock;
+      if (N >= kBlock || j < N) buf[j] = cmk(x[i], y[i]);
+    }
+  }
+};
+
+// Latency hiding: the next channel row is loaded into registers while the
+// current one is transformed, the template row and the rfft twiddles are in
+// registers before the FFT starts, the FFT twiddles and the per-channel
+// metadata sit in LDS (no global load inside the channel loop waits on the
+// prefetch), and the guess phasor e^{2 pi i k phi_n} advances by one
+// multiplication per 256 harmonics.  The per-channel sums are finished by
+// thread 0 after the row's last barrier.
 template <int LOGN>
 __global__ __launch_bounds__(kBlock) void k_data_xspec(SpecArgs a) {
   constexpr int N = 1 << LOGN;
   constexpr int NH = N + 1;
   constexpr int KI = (NH + kBlock - 1) / kBlock;
+  constexpr int NTW = 3 * N / 4;
   __shared__ double2 buf[N];
-  __shared__ double red[2 * kWaves];
+  __shared__ double2 twl[NTW];
+  __shared__ double red[2][2 * kWaves];
   __shared__ double s_meta[4];
+  extern __shared__ __align__(16) unsigned char dyn[];
+  double2* cmeta = reinterpret_cast<double2*>(dyn);  // (phi_g, weight or NaN if masked)
   const int c = blockIdx.x;
   const int s = a.sub0 + c;
   const int tid = threadIdx.x;
@@ -86,7 +125,17 @@ __global__ __launch_bounds__(kBlock) void k_data_xspec(SpecArgs a) {
   const int midx = a.model_idx ? a.model_idx[s] : 0;
   const double* fr = a.freqs + (size_t)s * nchan;
   const uint8_t* mask = a.mask ? a.mask + (size_t)s * nchan : nullptr;
+  const double* drow0 = a.data + (size_t)s * nchan * (2 * N);
 
+  RowRegs<LOGN> row;
+  row.load(drow0);  // row 0 in flight first
+  for (int e = tid; e < NTW; e += kBlock) twl[e] = a.tw[2 * e];
+  double2 twp[KI];
+#pragma unroll
+  for (int i = 0; i < KI; ++i) {
+    const int k = tid + i * kBlock;
+    twp[i] = a.tw[k <= N ? k : 0];
+  }
   // nu_g (guess dedispersion reference) default: mean over fitted channels
   if (tid == 0) {
     double fs = 0.0, ws = 0.0;
@@ -105,62 +154,77 @@ __global__ __launch_bounds__(kBlock) void k_data_xspec(SpecArgs a) {
     s_meta[3] = a.init ? a.init[(size_t)s * 5 + 1] : 0.0;
   }
   __syncthreads();
-  const double nug = s_meta[0];
   const double wsum = s_meta[1];
-  const double DMg = s_meta[3];
-  const double Pp = a.P[s];
-  const double Dfac = kDconst * DMg / Pp;
-  const double nug2 = 1.0 / (nug * nug);
+  {
+    const double nug = s_meta[0];
+    const double Dfac = kDconst * s_meta[3] / a.P[s];
+    const double nug2 = 1.0 / (nug * nug);
+    for (int n = tid; n < nchan; n += kBlock) {
+      const bool ok = !mask || mask[n];
+      const double w = a.weights ? a.weights[(size_t)s * nchan + n] : 1.0;
+      cmeta[n] = cmk(Dfac * (1.0 / (fr[n] * fr[n]) - nug2), ok ? w : NAN);
+    }
+  }
+  __syncthreads();
 
   double2 racc[KI];
 #pragma unroll
   for (int i = 0; i < KI; ++i) racc[i] = cmk(0.0, 0.0);
 
-  const double* drow0 = a.data + (size_t)s * nchan * (2 * N);
   for (int n = 0; n < nchan; ++n) {
     double2* Xr = a.X + ((size_t)c * nchan + n) * a.NHP;
-    if (mask && !mask[n]) {
+    const double2 cm = cmeta[n];
+    const bool ok = !isnan(cm.y);
+    if (ok) row.store(buf);
+    if (n + 1 < nchan) row.load(drow0 + (size_t)(n + 1) * 2 * N);
+    if (!ok) {
       for (int k = tid; k < a.NHP; k += kBlock) Xr[k] = cmk(0.0, 0.0);
       if (tid == 0) { a.sig[(size_t)c * nchan + n] = 0.0; a.dsum[(size_t)c * nchan + n] = 0.0; }
       continue;
     }
-    load_row<LOGN>(buf, drow0 + (size_t)n * 2 * N);
-    __syncthreads();
-    lds_fft<LOGN, false>(buf, a.tw);
     const double2* Mr = a.M + ((size_t)midx * nchan + n) * a.NHP;
-    const double w = a.weights ? a.weights[(size_t)s * nchan + n] : 1.0;
-    const double phig = Dfac * (1.0 / (fr[n] * fr[n]) - nug2);
+    double2 mreg[KI];
+#pragma unroll
+    for (int i = 0; i < KI; ++i) {
+      const int k = tid + i * kBlock;
+      mreg[i] = Mr[k <= N ? k : 0];
+    }
+    __syncthreads();
+    lds_fft_twl<LOGN>(buf, twl);
+    const double w = cm.y;
+    double2 ph = cmk(1.0, 0.0), phst = cmk(1.0, 0.0);
+    if (a.guess) {
+      ph = turn_phasor((double)tid, cm.x);
+      phst = turn_phasor((double)kBlock, cm.x);
+    }
     double pn = 0.0, pd = 0.0;
 #pragma unroll
     for (int i = 0; i < KI; ++i) {
       const int k = tid + i * kBlock;
+      if (i > 0) ph = cmul(ph, phst);
       if (k <= N) {
-        const double2 x = rfft_post<LOGN>(buf, k, a.tw);
+        const double2 x = rfft_post_w<LOGN>(buf, k, twp[i]);
         const double p2 = cabs2(x);
         if (k >= a.kc) pn += p2;
         if (k >= 1) pd += p2;
-        const double2 m = Mr[k];
-        Xr[k] = (k == 0) ? cmk(0.0, 0.0) : cmulc(x, m);
-        if (a.guess) {
-          racc[i] = cadd(racc[i], cscale(cmul(x, turn_phasor((double)k, phig)), w));
-        }
+        Xr[k] = (k == 0) ? cmk(0.0, 0.0) : cmulc(x, mreg[i]);
+        if (a.guess) racc[i] = cadd(racc[i], cscale(cmul(x, ph), w));
       }
     }
     for (int k = NH + tid; k < a.NHP; k += kBlock) Xr[k] = cmk(0.0, 0.0);
-    // two block sums with one barrier pair
     pn = wave_sum(pn);
     pd = wave_sum(pd);
-    if ((tid & 63) == 0) { red[tid >> 6] = pn; red[kWaves + (tid >> 6)] = pd; }
-    __syncthreads();
+    double* rd = red[n & 1];
+    if ((tid & 63) == 0) { rd[tid >> 6] = pn; rd[kWaves + (tid >> 6)] = pd; }
+    __syncthreads();  // buf and rd complete; the next row may overwrite buf
     if (tid == 0) {
       double sn = 0.0, sd = 0.0;
-      for (int i = 0; i < kWaves; ++i) { sn += red[i]; sd += red[kWaves + i]; }
-      double sig = a.errs ? a.errs[(size_t)s * nchan + n]
-                          : sqrt(sn / (double)(2 * N) / (double)(NH - a.kc));
+      for (int i = 0; i < kWaves; ++i) { sn += rd[i]; sd += rd[kWaves + i]; }
+      const double sig = a.errs ? a.errs[(size_t)s * nchan + n]
+                                : sqrt(sn / (double)(2 * N) / (double)(NH - a.kc));
       a.sig[(size_t)c * nchan + n] = sig;
       a.dsum[(size_t)c * nchan + n] = sd;
     }
-    __syncthreads();
   }
   if (a.guess) {
     double2* Rr = a.R + (size_t)c * a.NHP;

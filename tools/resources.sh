@@ -21,7 +21,7 @@ for ln in sys.stdin:
 for r in rows:
     if pat and not re.search(pat, r["name"]):
         continue
-    print("%-48s vgpr %4s sgpr-spill %3s scratch %5s occ %s lds %s" % (r["name"][:48], r.get("VGPRs"),
+    print("%-44s vgpr %4s vspill %3s sspill %3s scratch %5s occ %s lds %s" % (r["name"][:44], r.get("VGPRs"), r.get("VGPRs Spill"),
           r.get("SGPRs Spill"), r.get("ScratchSize [bytes/lane]"), r.get("Occupancy [waves/SIMD]"),
           r.get("LDS Size [bytes/block]")))
 ' "$1"
