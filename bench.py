@@ -145,7 +145,7 @@ def main():
 
     ktimes = {}
     if not args.no_timing:
-        for name in ["data_xspec", "guess", "solve", "post", "model_fft"]:
+        for name in ["data_xspec", "guess", "moments", "solve", "post", "model_fft"]:
             ms, n = eng.kernel_time(name)
             ktimes[name] = (ms, n)
         eng.set_timing(False)
@@ -173,6 +173,9 @@ def main():
         elif dom == "data_xspec":
             bytes_launch = nsub * (8.0 * nchan * nbin + 16.0 * nchan * nharm)
             what = "k_data_xspec: 8 B/sample read + 16 B/cell X written"
+        elif dom == "moments":
+            bytes_launch = nsub * 8.0 * nchan * nbin
+            what = "k_moments: 8 B/sample data re-read (Taylor moments, nothing written per cell)"
         elif dom == "post":
             bytes_launch = nsub * nchan * nharm * 16.0
             what = "k_post: one with-scales pass over X"
@@ -187,7 +190,8 @@ def main():
                 "traffic_source": os.path.relpath(PMC_TRAFFIC, ROOT) if traffic else None,
                 "avg_launch_ms": round(ms / max(n, 1), 4),
                 "algorithmic_bytes_per_launch": bytes_launch, "bytes_model": what,
-                "kernel_ms_per_step": {k: round(v[0] / max(v[1], 1), 4) for k, v in ktimes.items()}}
+                "kernel_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in ktimes.items()},
+                "kernel_launches_per_step": {k: round(v[1] / args.steps, 2) for k, v in ktimes.items()}}
 
     # ---- CPU baseline (oracle, 1 core) on a bounded sample + sample parity ----
     cpu = None

@@ -64,7 +64,8 @@ extern "C" {
 #define PPF_K_NOISE 8
 #define PPF_K_GUESS 9
 #define PPF_K_POST 10
-#define PPF_NUM_KERNELS 11
+#define PPF_K_MOMENTS 11
+#define PPF_NUM_KERNELS 12
 
 typedef struct ppf_ctx ppf_ctx;
 
@@ -88,6 +89,12 @@ int ppf_reset_kernel_times(ppf_ctx* ctx);
 /* ---------------------------------------------------------------------- */
 #define PPF_METHOD_TRUST_NCG 0
 
+/* Phase-family fits (tau = 0 and not fitted) evaluate the objective from
+ * per-channel Taylor moments of the cross-spectrum (no nchan x nharm
+ * workspace).  PPF_SOLVE_EXACT forces the exact cross-spectrum sweeps
+ * instead (same results to rounding; used to cross-check the two).       */
+#define PPF_SOLVE_EXACT 1
+
 typedef struct {
   int32_t nsub, nchan, nbin, nmodel;
   int32_t fit_flags[5];   /* phi, DM, GM, tau, alpha (pptoaslib.py:928)     */
@@ -98,7 +105,7 @@ typedef struct {
   int32_t guess;          /* 1: in-kernel initial phase guess (pptoas.py:420-456) */
   int32_t guess_Ns;       /* opt.brute grid size (100 in pptoas, nbin in ppalign) */
   int32_t guess_wrap;     /* 1: phase_transform(..., mod=True) to nu_fit_DM */
-  int32_t reserved;
+  int32_t solver_flags;   /* PPF_SOLVE_* bits (0 = default)                */
   const double* data;       /* [nsub][nchan][nbin]                          */
   const double* model;      /* [nmodel][nchan][nbin]                        */
   const int32_t* model_idx; /* [nsub] or NULL (all 0)                       */

@@ -14,7 +14,8 @@ PPF_OK = 0
 PPF_METHOD_TRUST_NCG = 0
 KERNEL_IDS = {"model_fft": 0, "data_xspec": 1, "solve": 2, "phase_shift": 3,
               "rotate": 4, "rot_accum": 5, "synth": 6, "irfft": 7, "noise": 8,
-              "guess": 9, "post": 10}
+              "guess": 9, "post": 10, "moments": 11}
+PPF_SOLVE_EXACT = 1
 
 _dp = ctypes.c_void_p  # device pointers travel as plain addresses
 
@@ -27,7 +28,7 @@ class FitDesc(ctypes.Structure):
                 ("log10_tau", ctypes.c_int32), ("option", ctypes.c_int32),
                 ("method", ctypes.c_int32), ("is_toa", ctypes.c_int32),
                 ("guess", ctypes.c_int32), ("guess_Ns", ctypes.c_int32),
-                ("guess_wrap", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("guess_wrap", ctypes.c_int32), ("solver_flags", ctypes.c_int32),
                 ("data", _dp), ("model", _dp), ("model_idx", _dp),
                 ("freqs", _dp), ("errs", _dp), ("chan_mask", _dp),
                 ("weights", _dp), ("P", _dp), ("init", _dp), ("nu_fit", _dp),

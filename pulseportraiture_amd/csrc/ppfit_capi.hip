@@ -38,6 +38,7 @@ struct ppf_ctx {
   Buffer ws;      // per-chunk fit workspace
   Buffer mspec;   // template spectra
   Buffer aux;     // misc (synth templates, partial sums)
+  Buffer mmean;   // mean template spectra (guess)
   bool timing = false;
   std::vector<TimedLaunch> pending;
   std::vector<hipEvent_t> pool;
@@ -219,6 +220,7 @@ void ppf_ctx_destroy(ppf_ctx* ctx) {
   if (ctx->ws.p) (void)hipFree(ctx->ws.p);
   if (ctx->mspec.p) (void)hipFree(ctx->mspec.p);
   if (ctx->aux.p) (void)hipFree(ctx->aux.p);
+  if (ctx->mmean.p) (void)hipFree(ctx->mmean.p);
   delete ctx;
 }
 
@@ -291,13 +293,43 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   if (int r = model_spectra(ctx, d->nmodel * nchan, nbin, d->model, 1, ctx->mspec, &M, &pn))
     return r;
 
+  // X (the exact cross-spectrum) is needed only when some subint is fitted
+  // with scattering (or when exact sweeps are forced); phase-family subints
+  // keep kMT Taylor moments per channel instead.
+  const bool exact = (d->solver_flags & PPF_SOLVE_EXACT) != 0;
+  bool need_x = exact || d->fit_flags[3] || d->fit_flags[4];
+  if (!need_x) {
+    std::vector<double> hinit((size_t)d->nsub * 5);
+    HIPCHK(ctx, hipMemcpyAsync(hinit.data(), d->init, hinit.size() * sizeof(double),
+                               hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    for (int64_t i = 0; i < d->nsub && !need_x; ++i) {
+      const double t3 = hinit[(size_t)i * 5 + 3];
+      const double tl = d->log10_tau ? std::pow(10.0, t3) : t3;
+      need_x = tl != 0.0;
+    }
+  }
+  const bool taylor = !exact;
+  // mean template spectrum for the unmasked guess
+  double2* Mmean = nullptr;
+  if (d->guess) {
+    if (int r = ensure(ctx, ctx->mmean, (size_t)d->nmodel * NHP * sizeof(double2))) return r;
+    Mmean = reinterpret_cast<double2*>(ctx->mmean.p);
+    if (int r = timed(ctx, PPF_K_MODEL_FFT, [&] {
+          hipLaunchKernelGGL(k_model_mean, dim3((NHP + 255) / 256, d->nmodel), dim3(256), 0,
+                             ctx->stream, M, Mmean, nchan, NHP);
+        }))
+      return r;
+  }
+
   // per-subint workspace layout
-  const size_t bX = (size_t)nchan * NHP * sizeof(double2);
+  const size_t bX = need_x ? (size_t)nchan * NHP * sizeof(double2) : 0;
+  const size_t bT = taylor ? (size_t)2 * nchan * (kMT * sizeof(double2) + sizeof(int)) : 0;
   const size_t bR = (size_t)NHP * sizeof(double2);
   const size_t bC = (size_t)nchan * sizeof(double);
   const size_t bAcc = (size_t)2 * nchan * 10 * sizeof(double);
   const size_t bW = (size_t)nchan * 8 * sizeof(double);
-  const size_t per_sub = bX + 2 * bR + 2 * bC + sizeof(SolveState) + bAcc + bW;
+  const size_t per_sub = bX + bT + 2 * bR + 2 * bC + sizeof(SolveState) + bAcc + bW + sizeof(int);
   int64_t chunk = ctx->ws_limit / (int64_t)(per_sub + 1024);
   if (chunk < 1) chunk = 1;
   if (chunk > d->nsub) chunk = d->nsub;
@@ -310,7 +342,10 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   const size_t offSt = align256(offDs + cs * bC);
   const size_t offAcc = align256(offSt + cs * sizeof(SolveState));
   const size_t offW = align256(offAcc + cs * bAcc);
-  const size_t total = align256(offW + cs * bW);
+  const size_t offT = align256(offW + cs * bW);
+  const size_t offL = align256(offT + cs * bT);
+  const size_t offN = align256(offL + cs * sizeof(int));
+  const size_t total = align256(offN + sizeof(int));
   if (int r = ensure(ctx, ctx->ws, total)) return r;
   char* base = static_cast<char*>(ctx->ws.p);
 
@@ -329,7 +364,10 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   sa.P = d->P;
   sa.init = d->init;
   sa.guess_nu = d->guess_nu;
-  sa.X = reinterpret_cast<double2*>(base + offX);
+  sa.log10_tau = d->log10_tau;
+  sa.fit_tau = d->fit_flags[3] ? 1 : 0;
+  sa.exact = exact ? 1 : 0;
+  sa.X = need_x ? reinterpret_cast<double2*>(base + offX) : nullptr;
   sa.R = reinterpret_cast<double2*>(base + offR);
   sa.sig = reinterpret_cast<double*>(base + offSig);
   sa.dsum = reinterpret_cast<double*>(base + offDs);
@@ -366,6 +404,15 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   fa.st = reinterpret_cast<SolveState*>(base + offSt);
   fa.acc = reinterpret_cast<double*>(base + offAcc);
   fa.wsc = reinterpret_cast<double*>(base + offW);
+  fa.T = taylor ? reinterpret_cast<double2*>(base + offT) : nullptr;
+  fa.Tcnt = taylor ? reinterpret_cast<int*>(base + offT + cs * 2 * nchan * kMT * sizeof(double2))
+                   : nullptr;
+  fa.data = d->data;
+  fa.tw = tw;
+  fa.Mmean = Mmean;
+  fa.rq_list = nullptr;
+  fa.rq_count = reinterpret_cast<int*>(base + offN);
+  int* rq_list = reinterpret_cast<int*>(base + offL);
   fa.o_params = o->params;
   fa.o_param_errs = o->param_errs;
   fa.o_nu_out = o->nu_out;
@@ -389,7 +436,7 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
     sa.sub0 = (int)s0;
     fa.sub0 = (int)s0;
     if (int r = timed(ctx, PPF_K_DATA_XSPEC, [&] {
-          LOGN_SWITCH(logN, hipLaunchKernelGGL(k_data_xspec<LG>, dim3(nc), dim3(kBlock), (size_t)nchan * sizeof(double2),
+          LOGN_SWITCH(logN, hipLaunchKernelGGL(k_data_xspec<LG>, dim3(nc), dim3(XspecCfg<LG>::WPB * 64), (size_t)nchan * sizeof(double2),
                                                ctx->stream, sa));
         }))
       return r;
@@ -398,12 +445,43 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
                              ctx->stream, fa);
         }))
       return r;
-    // each subint runs in exactly one of the phase-only / scattering variants
+    // each subint runs in exactly one of the phase-only / scattering /
+    // Taylor variants (the others exit at once)
     if (int r = timed(ctx, PPF_K_SOLVE, [&] {
-          hipLaunchKernelGGL(k_solve<false>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
-          hipLaunchKernelGGL(k_solve<true>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
+          if (!taylor)
+            hipLaunchKernelGGL(k_solve<false>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
+          if (need_x)
+            hipLaunchKernelGGL(k_solve<true>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
         }))
       return r;
+    if (taylor) {
+      FitArgs ma = fa;
+      int nlist = nc;
+      for (int round = 0;; ++round) {
+        if (round > 4000) return fail(ctx, PPF_ERR_DEVICE, "Taylor recentring did not settle");
+        if (int r = timed(ctx, PPF_K_MOMENTS, [&] {
+              LOGN_SWITCH(logN, hipLaunchKernelGGL(k_moments<LG>, dim3(nlist),
+                                                   dim3(MomentsCfg<LG>::WPB * 64), 0, ctx->stream,
+                                                   ma));
+            }))
+          return r;
+        HIPCHK(ctx, hipMemsetAsync(fa.rq_count, 0, sizeof(int), ctx->stream));
+        fa.rq_list = rq_list;
+        if (int r = timed(ctx, PPF_K_SOLVE, [&] {
+              hipLaunchKernelGGL(k_solve_taylor, dim3(nc), dim3(kBlock), lds_meta, ctx->stream,
+                                 fa);
+            }))
+          return r;
+        fa.rq_list = nullptr;
+        int hcount = 0;
+        HIPCHK(ctx, hipMemcpyAsync(&hcount, fa.rq_count, sizeof(int), hipMemcpyDeviceToHost,
+                                   ctx->stream));
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        if (hcount == 0) break;
+        ma.rq_list = rq_list;
+        nlist = hcount;
+      }
+    }
     if (int r = timed(ctx, PPF_K_POST, [&] {
           hipLaunchKernelGGL(k_post<false>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
           hipLaunchKernelGGL(k_post<true>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);

@@ -199,32 +199,46 @@ __device__ void lds_fft(double2* buf, const double2* __restrict__ tw) {
   }
 }
 
-// Forward FFT like lds_fft<LOGN, false>, with its twiddles read from an LDS
-// table twl[e] = e^{-2 pi i e / N}, e < 3N/4 (filled once per workgroup):
-// radix-4 pass with span Ns needs exponents r k N / (4 Ns) < 3N/4.
-template <int LOGN>
-__device__ __forceinline__ void lds_fft_twl(double2* buf, const double2* twl) {
+// Sync for the threads that share an LDS FFT buffer: the whole block, or one
+// wave (LDS operations of a wave execute in order; the wave barrier and the
+// fences only stop the compiler from moving LDS accesses across it).
+template <bool WAVE>
+__device__ __forceinline__ void fft_sync() {
+  if constexpr (WAVE) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  } else {
+    __syncthreads();
+  }
+}
+
+// Forward Stockham FFT of N = 2^LOGN points in buf by NT threads (t = 0..NT-1),
+// twiddles from an LDS table twl[e] = e^{-2 pi i e / N}, e < 3N/4 (radix-4
+// pass with span Ns needs exponents r k N / (4 Ns) < 3N/4).  WAVE: NT = 64
+// and buf is private to the calling wave.
+template <int LOGN, int NT, bool WAVE>
+__device__ __forceinline__ void stockham_twl(double2* buf, const double2* twl, int t) {
   constexpr int N = 1 << LOGN;
   constexpr int Q = N / 4;
-  constexpr int B4 = (Q + kBlock - 1) / kBlock;
-  const int tid = threadIdx.x;
+  constexpr int B4 = (Q + NT - 1) / NT;
   int Ns = 1;
   if constexpr (LOGN & 1) {
     constexpr int H = N / 2;
-    constexpr int B2 = (H + kBlock - 1) / kBlock;
+    constexpr int B2 = (H + NT - 1) / NT;
     double2 a[B2], b[B2];
 #pragma unroll
     for (int c = 0; c < B2; ++c) {
-      const int j = tid + c * kBlock;
+      const int j = t + c * NT;
       if (j < H) { a[c] = buf[j]; b[c] = buf[j + H]; }
     }
-    __syncthreads();
+    fft_sync<WAVE>();
 #pragma unroll
     for (int c = 0; c < B2; ++c) {
-      const int j = tid + c * kBlock;
+      const int j = t + c * NT;
       if (j < H) { buf[2 * j] = cadd(a[c], b[c]); buf[2 * j + 1] = csub(a[c], b[c]); }
     }
-    __syncthreads();
+    fft_sync<WAVE>();
     Ns = 2;
   }
 #pragma unroll
@@ -232,7 +246,7 @@ __device__ __forceinline__ void lds_fft_twl(double2* buf, const double2* twl) {
     double2 v[B4][4];
 #pragma unroll
     for (int c = 0; c < B4; ++c) {
-      const int j = tid + c * kBlock;
+      const int j = t + c * NT;
       if (j < Q) {
         const int k = j & (Ns - 1);
         const int e = k * (N / (4 * Ns));
@@ -241,10 +255,10 @@ __device__ __forceinline__ void lds_fft_twl(double2* buf, const double2* twl) {
         for (int r = 1; r < 4; ++r) v[c][r] = cmul(buf[j + r * Q], twl[r * e]);
       }
     }
-    __syncthreads();
+    fft_sync<WAVE>();
 #pragma unroll
     for (int c = 0; c < B4; ++c) {
-      const int j = tid + c * kBlock;
+      const int j = t + c * NT;
       if (j < Q) {
         radix4<false>(v[c][0], v[c][1], v[c][2], v[c][3]);
         const int k = j & (Ns - 1);
@@ -255,9 +269,110 @@ __device__ __forceinline__ void lds_fft_twl(double2* buf, const double2* twl) {
         buf[d + 3 * Ns] = v[c][3];
       }
     }
-    __syncthreads();
+    fft_sync<WAVE>();
     Ns *= 4;
   }
+}
+
+// Per-pass twiddle tables for the wave FFT.  A radix-4 pass of span Ns needs
+// w^{r k}, w = e^{-2 pi i / (4 Ns)}, k < Ns, r = 1..3.  Read from one table of
+// e^{-2 pi i e / N} they sit N / (4 Ns) entries apart, so the lanes of a pass
+// hit one LDS bank (up to 16-way conflicts); here each pass has its own
+// contiguous rows [r = 1][k], [r = 2][k] and w^{3k} = w^k w^{2k}.
+template <int LOGN>
+struct PassTw {
+  static constexpr int NP = LOGN / 2;                 // radix-4 passes
+  static constexpr int NS0 = (LOGN & 1) ? 2 : 1;      // span of the first one
+  static constexpr int span(int p) { return NS0 << (2 * p); }
+  static constexpr int off(int p) { return p == 0 ? 0 : off(p - 1) + 2 * span(p - 1); }
+  static constexpr int SIZE = off(NP);
+};
+
+// tpt[off(p) + (r-1) Ns + k] = e^{-2 pi i r k / (4 Ns)} from tw[m] = e^{-2 pi i m / (2N)}
+template <int LOGN>
+__device__ __forceinline__ void fill_pass_tw(double2* tpt, const double2* __restrict__ tw, int t,
+                                             int nt) {
+  using T = PassTw<LOGN>;
+  constexpr int N = 1 << LOGN;
+  for (int e = t; e < T::SIZE; e += nt) {
+    int p = 0;
+    while (p + 1 < T::NP && e >= T::off(p + 1)) ++p;
+    const int Ns = T::span(p);
+    const int q = e - T::off(p);
+    const int r = 1 + q / Ns, k = q % Ns;
+    tpt[e] = tw[r * k * (N / (2 * Ns))];
+  }
+}
+
+// Wave-synchronous forward Stockham FFT (64 lanes) with per-pass twiddles.
+template <int LOGN>
+__device__ __forceinline__ void wave_fft(double2* buf, const double2* tpt, int t) {
+  using T = PassTw<LOGN>;
+  constexpr int N = 1 << LOGN;
+  constexpr int NT = 64;
+  constexpr int Q = N / 4;
+  constexpr int B4 = (Q + NT - 1) / NT;
+  if constexpr (LOGN & 1) {
+    constexpr int H = N / 2;
+    constexpr int B2 = (H + NT - 1) / NT;
+    double2 a[B2], b[B2];
+#pragma unroll
+    for (int c = 0; c < B2; ++c) {
+      const int j = t + c * NT;
+      if (j < H) { a[c] = buf[j]; b[c] = buf[j + H]; }
+    }
+    fft_sync<true>();
+#pragma unroll
+    for (int c = 0; c < B2; ++c) {
+      const int j = t + c * NT;
+      if (j < H) { buf[2 * j] = cadd(a[c], b[c]); buf[2 * j + 1] = csub(a[c], b[c]); }
+    }
+    fft_sync<true>();
+  }
+#pragma unroll
+  for (int p = 0; p < T::NP; ++p) {
+    const int Ns = T::span(p);
+    const double2* tp = tpt + T::off(p);
+    double2 v[B4][4];
+#pragma unroll
+    for (int c = 0; c < B4; ++c) {
+      const int j = t + c * NT;
+      if (j < Q) {
+        const int k = j & (Ns - 1);
+        v[c][0] = buf[j];
+        if (Ns == 1) {
+#pragma unroll
+          for (int r = 1; r < 4; ++r) v[c][r] = buf[j + r * Q];
+        } else {
+          const double2 w1 = tp[k], w2 = tp[Ns + k];
+          v[c][1] = cmul(buf[j + Q], w1);
+          v[c][2] = cmul(buf[j + 2 * Q], w2);
+          v[c][3] = cmul(buf[j + 3 * Q], cmul(w1, w2));
+        }
+      }
+    }
+    fft_sync<true>();
+#pragma unroll
+    for (int c = 0; c < B4; ++c) {
+      const int j = t + c * NT;
+      if (j < Q) {
+        radix4<false>(v[c][0], v[c][1], v[c][2], v[c][3]);
+        const int k = j & (Ns - 1);
+        const int d = (j - k) * 4 + k;
+        buf[d] = v[c][0];
+        buf[d + Ns] = v[c][1];
+        buf[d + 2 * Ns] = v[c][2];
+        buf[d + 3 * Ns] = v[c][3];
+      }
+    }
+    fft_sync<true>();
+  }
+}
+
+// Block-wide forward FFT with LDS twiddles (all kBlock threads).
+template <int LOGN>
+__device__ __forceinline__ void lds_fft_twl(double2* buf, const double2* twl) {
+  stockham_twl<LOGN, kBlock, false>(buf, twl, threadIdx.x);
 }
 
 // rfft_post with the twiddle e^{-2 pi i k / 2N} passed in (a register).
@@ -293,6 +408,80 @@ __device__ __forceinline__ double2 irfft_pre(double2 xk, double2 xnk, int k, con
   const double2 e = cscale(cadd(xk, xc), 0.5);
   const double2 o = cmul(cscale(csub(xk, xc), 0.5), cconj(tw[k]));
   return cmk(e.x - o.y, e.y + o.x);  // e + i o
+}
+
+}  // namespace ppf
+
+namespace ppf {
+
+// ---------------------------------------------------------------------------
+// Wave-per-row streaming (k_data_xspec, k_moments): each wave owns one LDS
+// row buffer of N + 8 packed complex slots and walks its own channel list,
+// so the channel loop has no workgroup barrier.  Rows of N <= 1024 points
+// are prefetched into registers (16 doubles2 per lane) one channel ahead.
+// ---------------------------------------------------------------------------
+template <int LOGN>
+struct WaveRow {
+  static constexpr int N = 1 << LOGN;
+  static constexpr int LI = N >= 64 ? N / 64 : 1;
+  static constexpr bool kPrefetch = LOGN <= 10;
+  static constexpr int PL = kPrefetch ? LI : 1;
+  double x[PL], y[PL];
+  // global -> registers (prefetch form)
+  __device__ __forceinline__ void load(const double* __restrict__ src, int lane) {
+    if constexpr (kPrefetch) {
+      const double2* r2 = reinterpret_cast<const double2*>(src);
+#pragma unroll
+      for (int i = 0; i < LI; ++i) {
+        const int j = lane + 64 * i;
+        if (N >= 64 || j < N) {
+          const double2 v = r2[j];
+          x[i] = v.x;
+          y[i] = v.y;
+        }
+      }
+    }
+  }
+  // registers -> LDS (prefetch form) or global -> LDS directly
+  __device__ __forceinline__ void store(double2* buf, const double* __restrict__ src,
+                                        int lane) const {
+    if constexpr (kPrefetch) {
+#pragma unroll
+      for (int i = 0; i < LI; ++i) {
+        const int j = lane + 64 * i;
+        if (N >= 64 || j < N) buf[j] = cmk(x[i], y[i]);
+      }
+    } else {
+      const double2* r2 = reinterpret_cast<const double2*>(src);
+#pragma unroll 4
+      for (int i = 0; i < LI; ++i) buf[lane + 64 * i] = r2[lane + 64 * i];
+    }
+  }
+};
+
+// Spectrum pair of a real 2N-point row from its packed forward FFT Z in buf
+// (numpy rfft layout): for k in [0, N/2], w = e^{-i pi k / N},
+//   X_k = E + w O,  X_{N-k} = conj(E - w O),
+//   E = (Z_k + conj Z_{N-k}) / 2,  O = -i (Z_k - conj Z_{N-k}) / 2.
+// (k = 0 gives X_0 and X_N from Z_0; at k = N/2 both are X_{N/2}.)
+template <int LOGN>
+__device__ __forceinline__ void rfft_pair(const double2* buf, int k, double2 w, double2& Xk,
+                                          double2& Xnk) {
+  constexpr int N = 1 << LOGN;
+  const double2 zk = buf[k];
+  const double2 zc = cconj(buf[(N - k) & (N - 1)]);
+  const double2 E = cscale(cadd(zk, zc), 0.5);
+  const double2 dd = csub(zk, zc);
+  const double2 O = cmk(0.5 * dd.y, -0.5 * dd.x);
+  const double2 P = cmul(w, O);
+  Xk = cadd(E, P);
+  Xnk = cconj(csub(E, P));
+}
+
+// Channel walk of one wave: n = first, first + step, ... skipping masked.
+__device__ __forceinline__ int next_chan(int n, int step, int nchan, const uint8_t* mask) {
+  while (n < nchan && mask && !mask[n]) n += step;
+  return n;
 }
 
 }  // namespace ppf

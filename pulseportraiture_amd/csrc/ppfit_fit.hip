@@ -328,6 +328,104 @@ __device__ __forceinline__ double phase_frac(const double* prm, double fr, const
   return ph - floor(ph);
 }
 
+// phi_n before reduction (pptoaslib.py:206-208)
+__device__ __forceinline__ double phase_full(const double* prm, double fr, const double* refs,
+                                             double P) {
+  const double f2 = 1.0 / (fr * fr);
+  const double r0 = 1.0 / (refs[0] * refs[0]);
+  const double r1 = 1.0 / (refs[1] * refs[1]);
+  return prm[0] + kDconst * prm[1] * (f2 - r0) / P + kDconst2 * prm[2] * (f2 * f2 - r1 * r1) / P;
+}
+
+// ---------------------------------------------------------------------------
+// Taylor-moment evaluation of one channel (ppfit_taylor.hip builds T).
+// With W_k = X_k e^{2 pi i k phi_c} and v_k = k / Ks, the sums the exact
+// sweep forms at phi_c + delta are, for y = 2 pi Ks delta,
+//   G_p = sum_k k^p W_k e^{2 pi i k delta} = Ks^p sum_m (i y)^m / m! T_{m+p}.
+// (Moments about v = 0, not the band centre: pulse spectra sit at low k, and
+// a centred expansion would cancel catastrophically in G_1, G_2.)
+// Lane h of the channel's 8 lanes takes m = h, h+8, ... (< kMTerm); the
+// result is linear in the partial series, so each lane returns its partial
+// acc and the caller's group8_sum completes it exactly as for cells_phase.
+// ---------------------------------------------------------------------------
+__constant__ double c_inv_fact[kMT] = {
+    1.0, 1.0, 0.5, 0.16666666666666666,
+    0.041666666666666664, 0.008333333333333333, 0.001388888888888889, 0.0001984126984126984,
+    2.48015873015873e-05, 2.7557319223985893e-06, 2.755731922398589e-07, 2.505210838544172e-08,
+    2.08767569878681e-09, 1.6059043836821613e-10, 1.1470745597729725e-11, 7.647163731819816e-13,
+    4.779477332387385e-14, 2.8114572543455206e-15, 1.5619206968586225e-16, 8.22063524662433e-18,
+    4.110317623312165e-19, 1.9572941063391263e-20, 8.896791392450574e-22, 3.8681701706306835e-23,
+    1.6117375710961184e-24, 6.446950284384474e-26, 2.4795962632247972e-27, 9.183689863795546e-29,
+    3.279889237069838e-30, 1.1309962886447718e-31, 3.7699876288159054e-33, 1.2161250415535181e-34};
+
+struct TaylorSrc {
+  const double2* T;    // this subint's moment rows for one centre: [nchan][kMT], or null (exact)
+  const int* cnt;      // [nchan] moments stored per row
+  const double* xc;    // centre params
+  const double* refc;  // centre reference frequencies
+};
+
+// offset of phi_n(prm, refs) from the centre's phi_n, reduced to [-1/2, 1/2]
+__device__ __forceinline__ double taylor_delta(const double* prm, const double* refs,
+                                               const TaylorSrc& ts, double fr, double P) {
+  double d = phase_full(prm, fr, refs, P) - phase_full(ts.xc, fr, ts.refc, P);
+  return d - rint(d);
+}
+
+__device__ __forceinline__ void taylor_cells(const double2* __restrict__ Tn, int cnt, int h,
+                                             double d, double Ks, double* acc) {
+  const int mterm = cnt - 2;  // terms of the series (T up to index cnt - 1)
+  const double y = kTwoPi * Ks * d;
+  double yh = 1.0;
+  for (int i = 0; i < h; ++i) yh *= y;
+  const double y2 = y * y, y4 = y2 * y2, y8 = y4 * y4;
+  double2 S0 = cmk(0.0, 0.0), S1 = S0, S2 = S0;
+  double ym = yh;
+#pragma unroll
+  for (int q = 0; q < (kMTerm + 7) / 8; ++q) {
+    const int m = h + 8 * q;
+    if (m < mterm) {
+      const double cf = ym * c_inv_fact[m];
+      const double2 t0 = Tn[m], t1 = Tn[m + 1], t2 = Tn[m + 2];
+      S0 = cmk(fma(cf, t0.x, S0.x), fma(cf, t0.y, S0.y));
+      S1 = cmk(fma(cf, t1.x, S1.x), fma(cf, t1.y, S1.y));
+      S2 = cmk(fma(cf, t2.x, S2.x), fma(cf, t2.y, S2.y));
+    }
+    ym *= y8;
+  }
+  // i^m = i^h for every m of this lane (m = h mod 4): only the parts the
+  // sweep needs, Re G_0, Im G_1, Re G_2
+  double r0, i1, r2;
+  switch (h & 3) {
+    case 1: r0 = -S0.y; i1 = S1.x; r2 = -S2.y; break;
+    case 2: r0 = -S0.x; i1 = -S1.y; r2 = -S2.x; break;
+    case 3: r0 = S0.y; i1 = -S1.x; r2 = S2.y; break;
+    default: r0 = S0.x; i1 = S1.y; r2 = S2.x; break;
+  }
+  acc[0] = r0;
+  acc[1] = Ks * i1;
+  acc[2] = (Ks * Ks) * r2;
+  for (int i = 3; i < NACC; ++i) acc[i] = 0.0;
+}
+
+// Largest |y_n| of the fitted channels for evaluating prm (at refs) from the
+// centre ts; every thread gets it.  red: >= kWaves doubles of LDS.
+__device__ double taylor_reach(const Meta& m, const double* prm, const double* refs,
+                               const TaylorSrc& ts, double P, double Ks, double* red) {
+  double mx = 0.0;
+  for (int j = threadIdx.x; j < m.nok; j += kBlock)
+    mx = fmax(mx, fabs(taylor_delta(prm, refs, ts, m.fr[j], P)));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) red[w] = mx;
+  __syncthreads();
+  double r = red[0];
+  for (int i = 1; i < kWaves; ++i) r = fmax(r, red[i]);
+  __syncthreads();
+  return kTwoPi * Ks * r;
+}
+
 // One sweep over all fitted channels at (prm, refs).  MODE 0: f, g, H for
 // the solver (out[0..20]) and raw accumulators into acc_slot; MODE 1: the
 // with-scales Hessian pieces (out[0..29]) and per-channel wsc rows.  SCAT
@@ -339,7 +437,7 @@ __device__ __forceinline__ double phase_frac(const double* prm, double fr, const
 template <int MODE, bool SCAT>
 __device__ void sweep(const FitArgs& a, const Meta& m, int c, int s, const double* prm,
                       const double* refs, double P, double* acc_slot, double* out,
-                      double (*red)[48]) {
+                      double (*red)[48], const TaylorSrc& ts) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g8 = lane >> 3, h = lane & 7;
   const int J = a.NHP >> 3;
@@ -357,12 +455,17 @@ __device__ void sweep(const FitArgs& a, const Meta& m, int c, int s, const doubl
     const int jj = valid ? j : m.nok - 1;
     const int n = m.chan[jj];
     const double fr = m.fr[jj];
-    const double phif = phase_frac(prm, fr, refs, P);
-    const double2* Xr = a.X + ((size_t)c * a.nchan + n) * a.NHP;
     double acc[NACC];
-    if (!scat) {
+    if (!SCAT && ts.T) {
+      taylor_cells(ts.T + (size_t)n * kMT, ts.cnt[n], h, taylor_delta(prm, refs, ts, fr, P),
+                   0.5 * (double)a.nbin, acc);
+    } else if (!scat) {
+      const double phif = phase_frac(prm, fr, refs, P);
+      const double2* Xr = a.X + ((size_t)c * a.nchan + n) * a.NHP;
       cells_phase(Xr, J, h, phif, acc);
     } else {
+      const double phif = phase_frac(prm, fr, refs, P);
+      const double2* Xr = a.X + ((size_t)c * a.nchan + n) * a.NHP;
       const double2* Mr = a.M + ((size_t)midx * a.nchan + n) * a.NHP;
       const double taun = tau_lin * pow(fr / refs[2], prm[4]);
       cells_scat(Xr, Mr, J, h, phif, taun, acc);
@@ -458,10 +561,19 @@ __global__ __launch_bounds__(kBlock) void k_guess(FitArgs a) {
     const double tl = a.log10_tau ? pow(10.0, st.x[3]) : st.x[3];
     st.scat = (tl != 0.0) || a.flags[3];
     st.scat_post = st.scat;
+    st.taylor = !st.scat && a.T != nullptr;
+    st.kit = 0;
+    st.phase = 0;
+    st.fin = 0;
+    st.mvalid = 0;
+    st.xslot = 0;
+    st.wslot = 0;
+    st.tr = 1.0;
   }
   if (!a.guess) {
     __syncthreads();
-    if (tid == 0) for (int i = 0; i < 5; ++i) st.init[i] = st.x[i];
+    if (tid == 0)
+      for (int i = 0; i < 5; ++i) { st.init[i] = st.x[i]; st.xc[0][i] = st.x[i]; }
     return;
   }
   // rm_k = R_k conj(Mm_k B_k(tau_g)): the guess template is irfft(B rfft(mean
@@ -479,9 +591,13 @@ __global__ __launch_bounds__(kBlock) void k_guess(FitArgs a) {
     // modelx.mean(axis=0) over the fitted channels (pptoas.py:454); its
     // spectrum is the mean of the DC-zeroed channel spectra.
     double2 mm = cmk(0.0, 0.0);
-    for (int n = 0; n < nchan; ++n)
-      if (!mask || mask[n]) mm = cadd(mm, Mb[(size_t)n * a.NHP + k]);
-    mm = cscale(mm, inv_cnt);
+    if (!mask && a.Mmean) {
+      mm = a.Mmean[(size_t)midx * a.NHP + k];
+    } else {
+      for (int n = 0; n < nchan; ++n)
+        if (!mask || mask[n]) mm = cadd(mm, Mb[(size_t)n * a.NHP + k]);
+      mm = cscale(mm, inv_cnt);
+    }
     if (k == N) mm.y = 0.0;
     if (tg != 0.0) {
       const double aa = kTwoPi * (double)k * tg;
@@ -508,9 +624,22 @@ __global__ __launch_bounds__(kBlock) void k_guess(FitArgs a) {
                  (pow(st.refs[0], -2.0) - pow(nug, -2.0)));
     if (a.guess_wrap) phi = wrap_half(phi);
     st.x[0] = phi;
-    for (int i = 0; i < 5; ++i) st.init[i] = st.x[i];
+    for (int i = 0; i < 5; ++i) { st.init[i] = st.x[i]; st.xc[0][i] = st.x[i]; }
   }
   (void)s_v;
+}
+
+// Mean of the DC-zeroed channel spectra of each template (unmasked guess
+// template, pptoas.py:454): Mmean[t][k] = sum_n M[t][n][k] / nchan.
+__global__ void k_model_mean(const double2* __restrict__ M, double2* __restrict__ Mmean, int nchan,
+                             int NHP) {
+  const int t = blockIdx.y;
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= NHP) return;
+  const double2* Mt = M + (size_t)t * nchan * NHP;
+  double2 mm = cmk(0.0, 0.0);
+  for (int n = 0; n < nchan; ++n) mm = cadd(mm, Mt[(size_t)n * NHP + k]);
+  Mmean[(size_t)t * NHP + k] = cscale(mm, 1.0 / (double)nchan);
 }
 
 // ---------------------------------------------------------------------------
@@ -628,7 +757,7 @@ __global__ __launch_bounds__(kBlock) void k_solve(FitArgs a) {
     }
   };
   if (!sh.done) {
-    sweep<0, SCAT>(a, m, c, s, sh.x, refs, P, acc0, sh.out, sh.red);
+    sweep<0, SCAT>(a, m, c, s, sh.x, refs, P, acc0, sh.out, sh.red, TaylorSrc{});
     if (tid < 64) {
       load_fgh(f, g, Hrow);
       xl = lane < 5 ? sh.x[lane] : 0.0;
@@ -651,7 +780,7 @@ __global__ __launch_bounds__(kBlock) void k_solve(FitArgs a) {
     if (sh.done) break;
     // every wave writes the proposal into the half the accepted point is not in
     double* sl = acc0 + (size_t)(sh.slot ^ 1) * a.nchan * NACC;
-    sweep<0, SCAT>(a, m, c, s, sh.xp, refs, P, sl, sh.out, sh.red);
+    sweep<0, SCAT>(a, m, c, s, sh.xp, refs, P, sl, sh.out, sh.red, TaylorSrc{});
     if (tid < 64) {
       double fp, gp, Hp[5] = {0, 0, 0, 0, 0};
       load_fgh(fp, gp, Hp);
@@ -1065,7 +1194,24 @@ __global__ __launch_bounds__(kBlock) void k_post(FitArgs a) {
   }
   __syncthreads();
   // ---- with-scales Hessian at the output parameters ----
-  sweep<1, SCAT>(a, m, c, s, sh.prm, sh.nu, P, nullptr, sh.out, sh.red);
+  // Taylor-path subints: the output params give the same phi_n (mod 1) as the
+  // accepted point, so the centre that evaluated it covers them too.
+  TaylorSrc ts{};
+  if (!SCAT && st.taylor) {
+    const double Ks = 0.5 * (double)a.nbin;
+    int best = st.xslot;
+    double by = INFINITY;
+    for (int q = 0; q < 2; ++q) {
+      if (!(st.mvalid & (1 << q))) continue;
+      const TaylorSrc tq{a.T + ((size_t)c * 2 + q) * nchan * kMT,
+                         a.Tcnt + ((size_t)c * 2 + q) * nchan, st.xc[q], st.refs};
+      const double y = taylor_reach(m, sh.prm, sh.nu, tq, P, Ks, sh.red[0]);
+      if (y < by) { by = y; best = q; }
+    }
+    ts = TaylorSrc{a.T + ((size_t)c * 2 + best) * nchan * kMT,
+                   a.Tcnt + ((size_t)c * 2 + best) * nchan, st.xc[best], st.refs};
+  }
+  sweep<1, SCAT>(a, m, c, s, sh.prm, sh.nu, P, nullptr, sh.out, sh.red, ts);
   if (tid == 0) {
     const int nf = sh.nfit;
     double A[25];

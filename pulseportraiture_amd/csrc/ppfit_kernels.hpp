@@ -9,6 +9,7 @@ namespace ppf {
 // ---------------------------------------------------------------------------
 struct SpecArgs {
   int sub0, nchan, NHP, kc, guess;
+  int log10_tau, fit_tau, exact;  // X is written only for subints that need it
   const double* data;      // [nsub][nchan][nbin]
   const double2* M;        // [nmodel][nchan][NHP] DC-zeroed template spectra
   const int* model_idx;    // [nsub] or null
@@ -37,13 +38,28 @@ struct PhaseShiftArgs {
   const double2* tw;
 };
 
+// Taylor-moment cross-spectrum (phase-family fits, see ppfit_taylor.hip):
+// kMT moments T_m = sum_k v_k^m W_k per channel, v_k = k / N in [0, 1]; an
+// evaluation at per-channel offset y = 2 pi N delta uses terms m < kMTerm and
+// is accepted while |y| <= kTaylorY, where the truncation
+// kTaylorY^kMTerm / kMTerm! e^kTaylorY is < 2e-17 of sum_k |W_k|.
+constexpr int kMT = 32;
+constexpr int kMTerm = kMT - 2;
+constexpr double kTaylorY = 3.0;
+
 // Per-subint solver state handed from k_guess -> k_solve -> k_post (global).
 struct SolveState {
   double x[5];     // current / final parameters
   double init[5];  // starting point (after the guess)
   double fun;
   double refs[3];  // nu_fit (resolved)
-  int nfev, status, slot, scat, scat_post, pad;
+  // Taylor path: expansion centres (params at refs), and the trust-ncg state
+  // saved when a proposal leaves both centres' radius (resumed after
+  // k_moments recentres)
+  double xc[2][5];
+  double g[5], H[25], tr;
+  int nfev, status, slot, scat, scat_post, taylor;
+  int kit, phase, fin, mvalid, xslot, wslot;
 };
 
 struct FitArgs {
@@ -66,6 +82,13 @@ struct FitArgs {
   const double* guess_nu;    // [nsub] or null
   const double* guess_tau;   // [nsub] or null
   SolveState* st;            // chunk [c]
+  double2* T;                // chunk [c][2][nchan][kMT] Taylor moments
+  int* Tcnt;                 // chunk [c][2][nchan] moments stored per row
+  const double* data;        // [nsub][nchan][nbin] (k_moments)
+  const double2* tw;         // rfft twiddles e^{-2 pi i m / nbin}
+  const double2* Mmean;      // [nmodel][NHP] mean template spectrum or null
+  int* rq_list;              // chunk: subints waiting for a recentre
+  int* rq_count;
   double* acc;               // chunk [c][2][nchan][10]
   double* wsc;               // chunk [c][nchan][8]
   // outputs (global batch index sub0 + c)
@@ -231,6 +254,9 @@ __global__ void k_rot_accum(const double* data, const double* phase, const doubl
                             const double2* tw);
 __global__ void k_accum_reduce(const double2* partial, double2* accum, int nsplit, size_t count);
 __global__ void k_guess(FitArgs a);
+__global__ void k_model_mean(const double2* M, double2* Mmean, int nchan, int NHP);
+template <int LOGN> __global__ void k_moments(FitArgs a);
+__global__ void k_solve_taylor(FitArgs a);
 template <bool SCAT> __global__ void k_solve(FitArgs a);
 template <bool SCAT> __global__ void k_post(FitArgs a);
 

@@ -1,4 +1,5 @@
 // ppfit_lib.hip -- single translation unit for libppfit.so (gfx950).
 #include "ppfit_spectra.hip"
 #include "ppfit_fit.hip"
+#include "ppfit_taylor.hip"
 #include "ppfit_capi.hip"

@@ -64,86 +64,72 @@ __global__ __launch_bounds__(kBlock) void k_model_spec(const double* __restrict_
 }
 
 // ---------------------------------------------------------------------------
-// Per-subint data pass.  For each fitted channel: rfft in LDS, then
-//   X[c][n][k]  = D_nk conj(M_nk)      (k >= 1; DC = 0; pad = 0)
+// Per-subint data pass.  For each fitted channel: rfft, then
 //   sig[c][n]   = errs[s][n] or sqrt(mean_{k>=kc} |D_k|^2 / nbin)
 //   dsum[c][n]  = sum_{k>=1} |D_k|^2
 //   R[c][k]    += w_n D_nk e^{2 pi i k phi_n},  phi_n = Dconst DM (nu_n^-2 -
 //                 nu_g^-2) / P  (rotate_data with DM, pplib.py:2406-2415)
+//   X[c][n][k]  = D_nk conj(M_nk)   only for subints fitted with the exact
+//                 (scattering) sweeps; phase-family subints get Taylor
+//                 moments from k_moments instead (ppfit_taylor.hip)
+// Channels go in groups of WPB: wave w transforms channel g*WPB + w in its
+// own LDS buffer (wave-synchronous Stockham, next row already in registers)
+// and post-processes the spectrum in (k, N-k) pairs straight from the packed
+// FFT, leaving its weighted, rotated spectrum in the buffer.  One barrier per
+// group, then every thread adds the group's WPB rows, in channel order, into
+// the R harmonics it owns (k = tid + nthr q, in registers).
 // ---------------------------------------------------------------------------
-// Row prefetch into registers, kept as plain doubles (a double2 array
-// carried across the channel loop is copied with memcpy and lands in scratch).
 template <int LOGN>
-struct RowRegs {
+struct XspecCfg {
   static constexpr int N = 1 << LOGN;
-  static constexpr int LI = N >= kBlock ? N / kBlock : 1;
-  double x[LI], y[LI];
-  __device__ __forceinline__ void load(const double* __restrict__ src) {
-    const double2* r2 = reinterpret_cast<const double2*>(src);
-#pragma unroll
-    for (int i = 0; i < LI; ++i) {
-      const int j = threadIdx.x + i * kBlock;
-      if (N >= kBlock || j < N) {
-        const double2 v = r2[j];
-        x[i] = v.x;
-        y[i] = v.y;
-      }
-    }
-  }
-  __device__ __forceinline__ void store(double2* buf) const {
-#pragma unroll
-    for (int i = 0; i < LI; ++i) {
-      const int j = threadIdx.x + i * kBlock;
-      if (N >= kBlock || j < N) buf[j] = cmk(x[i], y[i]);
-    }
-  }
+  // rows above 1024 points: one wave per workgroup, R accumulated in place
+  // in the subint's global R row (too large for registers)
+  static constexpr bool RREG = LOGN <= 10;
+  static constexpr int WPB = RREG ? 4 : 1;
+  static constexpr int NB = N + 8;                       // row buffer slots
+  static constexpr int NPI = (N / 2 + 1 + 63) / 64;      // pair iterations (k <= N/2)
+  static constexpr int NRQ = RREG ? (N + 1 + WPB * 64 - 1) / (WPB * 64) : 1;  // R slots/thread
 };
 
-// Latency hiding: the next channel row is loaded into registers while the
-// current one is transformed, the template row and the rfft twiddles are in
-// registers before the FFT starts, the FFT twiddles and the per-channel
-// metadata sit in LDS (no global load inside the channel loop waits on the
-// prefetch), and the guess phasor e^{2 pi i k phi_n} advances by one
-// multiplication per 256 harmonics.  The per-channel sums are finished by
-// thread 0 after the row's last barrier.
 template <int LOGN>
-__global__ __launch_bounds__(kBlock) void k_data_xspec(SpecArgs a) {
-  constexpr int N = 1 << LOGN;
+__global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
+  using Cfg = XspecCfg<LOGN>;
+  constexpr int N = Cfg::N;
   constexpr int NH = N + 1;
-  constexpr int KI = (NH + kBlock - 1) / kBlock;
-  constexpr int NTW = 3 * N / 4;
-  __shared__ double2 buf[N];
+  constexpr int WPB = Cfg::WPB;
+  constexpr int NPI = Cfg::NPI;
+  constexpr int NTW = PassTw<LOGN>::SIZE;
+  constexpr bool RREG = Cfg::RREG;
+  constexpr int nthr = WPB * 64;
+  __shared__ double2 bufs[WPB][Cfg::NB];
   __shared__ double2 twl[NTW];
-  __shared__ double red[2][2 * kWaves];
   __shared__ double s_meta[4];
+  __shared__ int s_act[WPB];
   extern __shared__ __align__(16) unsigned char dyn[];
   double2* cmeta = reinterpret_cast<double2*>(dyn);  // (phi_g, weight or NaN if masked)
   const int c = blockIdx.x;
   const int s = a.sub0 + c;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int nchan = a.nchan;
   const int midx = a.model_idx ? a.model_idx[s] : 0;
   const double* fr = a.freqs + (size_t)s * nchan;
   const uint8_t* mask = a.mask ? a.mask + (size_t)s * nchan : nullptr;
   const double* drow0 = a.data + (size_t)s * nchan * (2 * N);
+  double2* buf = bufs[w];
+  auto active = [&](int q) { return q < nchan && (!mask || mask[q]); };
 
-  RowRegs<LOGN> row;
-  row.load(drow0);  // row 0 in flight first
-  for (int e = tid; e < NTW; e += kBlock) twl[e] = a.tw[2 * e];
-  double2 twp[KI];
-#pragma unroll
-  for (int i = 0; i < KI; ++i) {
-    const int k = tid + i * kBlock;
-    twp[i] = a.tw[k <= N ? k : 0];
-  }
+  WaveRow<LOGN> row;
+  bool have = active(w);  // the registers hold (or are loading) this wave's next row
+  if (have) row.load(drow0 + (size_t)w * 2 * N, lane);  // first row in flight
+  fill_pass_tw<LOGN>(twl, a.tw, tid, nthr);
   // nu_g (guess dedispersion reference) default: mean over fitted channels
   if (tid == 0) {
     double fs = 0.0, ws = 0.0;
     int nok = 0;
-    for (int n = 0; n < nchan; ++n) {
-      if (mask && !mask[n]) continue;
-      fs += fr[n];
-      ws += a.weights ? a.weights[(size_t)s * nchan + n] : 1.0;
+    for (int q = 0; q < nchan; ++q) {
+      if (mask && !mask[q]) continue;
+      fs += fr[q];
+      ws += a.weights ? a.weights[(size_t)s * nchan + q] : 1.0;
       ++nok;
     }
     double nug = a.guess_nu ? a.guess_nu[s] : NAN;
@@ -155,90 +141,149 @@ __global__ __launch_bounds__(kBlock) void k_data_xspec(SpecArgs a) {
   }
   __syncthreads();
   const double wsum = s_meta[1];
+  // X is needed only by the exact (scattering) sweeps
+  bool wx = a.X != nullptr;
+  if (wx && !a.exact) {
+    const double t3 = a.init[(size_t)s * 5 + 3];
+    const double tl = a.log10_tau ? pow(10.0, t3) : t3;
+    wx = (tl != 0.0) || a.fit_tau;
+  }
   {
     const double nug = s_meta[0];
     const double Dfac = kDconst * s_meta[3] / a.P[s];
     const double nug2 = 1.0 / (nug * nug);
-    for (int n = tid; n < nchan; n += kBlock) {
-      const bool ok = !mask || mask[n];
-      const double w = a.weights ? a.weights[(size_t)s * nchan + n] : 1.0;
-      cmeta[n] = cmk(Dfac * (1.0 / (fr[n] * fr[n]) - nug2), ok ? w : NAN);
+    for (int q = tid; q < nchan; q += nthr) {
+      const bool ok = !mask || mask[q];
+      const double wq = a.weights ? a.weights[(size_t)s * nchan + q] : 1.0;
+      cmeta[q] = cmk(Dfac * (1.0 / (fr[q] * fr[q]) - nug2), ok ? wq : NAN);
     }
   }
-  __syncthreads();
+  double2 rq[Cfg::NRQ];  // R harmonics owned by this thread (RREG)
+#pragma unroll
+  for (int q = 0; q < Cfg::NRQ; ++q) rq[q] = cmk(0.0, 0.0);
+  double2* Rr = a.R + (size_t)c * a.NHP;
+  if (!RREG && a.guess)
+    for (int k = tid; k < a.NHP; k += nthr) Rr[k] = cmk(0.0, 0.0);
+  double sw, cw;
+  sincospi(-(double)lane / (double)N, &sw, &cw);
+  const double2 w0 = cmk(cw, sw);                    // e^{-i pi lane / N}
+  double ss, cs;
+  sincospi(-64.0 / (double)N, &ss, &cs);
+  const double2 wstep = cmk(cs, ss);                 // e^{-i pi 64 / N}
+  __syncthreads();  // twl, cmeta
 
-  double2 racc[KI];
-#pragma unroll
-  for (int i = 0; i < KI; ++i) racc[i] = cmk(0.0, 0.0);
-
-  for (int n = 0; n < nchan; ++n) {
-    double2* Xr = a.X + ((size_t)c * nchan + n) * a.NHP;
-    const double2 cm = cmeta[n];
-    const bool ok = !isnan(cm.y);
-    if (ok) row.store(buf);
-    if (n + 1 < nchan) row.load(drow0 + (size_t)(n + 1) * 2 * N);
-    if (!ok) {
-      for (int k = tid; k < a.NHP; k += kBlock) Xr[k] = cmk(0.0, 0.0);
-      if (tid == 0) { a.sig[(size_t)c * nchan + n] = 0.0; a.dsum[(size_t)c * nchan + n] = 0.0; }
-      continue;
+  const int ngroups = (nchan + WPB - 1) / WPB;
+  for (int g = 0; g < ngroups; ++g) {
+    const int n = g * WPB + w;
+    const bool act = active(n);
+    if (lane == 0) s_act[w] = act;
+    if (act && !have) row.load(drow0 + (size_t)n * 2 * N, lane);
+    have = false;
+    if (act) {
+      row.store(buf, drow0 + (size_t)n * 2 * N, lane);
     }
-    const double2* Mr = a.M + ((size_t)midx * nchan + n) * a.NHP;
-    double2 mreg[KI];
-#pragma unroll
-    for (int i = 0; i < KI; ++i) {
-      const int k = tid + i * kBlock;
-      mreg[i] = Mr[k <= N ? k : 0];
+    if (active(n + WPB)) {
+      row.load(drow0 + (size_t)(n + WPB) * 2 * N, lane);
+      have = true;
     }
-    __syncthreads();
-    lds_fft_twl<LOGN>(buf, twl);
-    const double w = cm.y;
-    double2 ph = cmk(1.0, 0.0), phst = cmk(1.0, 0.0);
-    if (a.guess) {
-      ph = turn_phasor((double)tid, cm.x);
-      phst = turn_phasor((double)kBlock, cm.x);
-    }
-    double pn = 0.0, pd = 0.0;
-#pragma unroll
-    for (int i = 0; i < KI; ++i) {
-      const int k = tid + i * kBlock;
-      if (i > 0) ph = cmul(ph, phst);
-      if (k <= N) {
-        const double2 x = rfft_post_w<LOGN>(buf, k, twp[i]);
-        const double p2 = cabs2(x);
-        if (k >= a.kc) pn += p2;
-        if (k >= 1) pd += p2;
-        Xr[k] = (k == 0) ? cmk(0.0, 0.0) : cmulc(x, mreg[i]);
-        if (a.guess) racc[i] = cadd(racc[i], cscale(cmul(x, ph), w));
+    if (act) {
+      fft_sync<true>();
+      wave_fft<LOGN>(buf, twl, lane);
+      const double2 cm = cmeta[n];
+      const double wgt = cm.y;
+      double2 e = cmk(1.0, 0.0), estep = e, EN = e;
+      if (a.guess) {
+        e = turn_phasor((double)lane, cm.x);
+        estep = turn_phasor(64.0, cm.x);
+        EN = turn_phasor((double)N, cm.x);
+      }
+      const double2* Mr = a.M + ((size_t)midx * nchan + n) * a.NHP;
+      double2* Xr = wx ? a.X + ((size_t)c * nchan + n) * a.NHP : nullptr;
+      double pn = 0.0, pd = 0.0;
+      double2 tw = w0;
+#pragma unroll 1
+      for (int i = 0; i < NPI; ++i) {
+        const int k = lane + 64 * i;
+        if (i > 0) { tw = cmul(tw, wstep); e = cmul(e, estep); }
+        if (k <= N / 2) {
+          double2 xk, xn;
+          rfft_pair<LOGN>(buf, k, tw, xk, xn);
+          const int kn = N - k;
+          const double p2k = cabs2(xk), p2n = cabs2(xn);
+          const bool two = k < N / 2;  // k = N/2 is its own partner
+          if (k >= a.kc) pn += p2k;
+          if (two && kn >= a.kc) pn += p2n;
+          if (k >= 1) pd += p2k;
+          if (two) pd += p2n;
+          if (wx) {
+            Xr[k] = (k == 0) ? cmk(0.0, 0.0) : cmulc(xk, Mr[k]);
+            if (two) Xr[kn] = cmulc(xn, Mr[kn]);
+          }
+          if (a.guess) {
+            // e^{2 pi i (N-k) phi} = e^{2 pi i N phi} conj(e^{2 pi i k phi});
+            // the pair's two slots are read and written by this lane only
+            const double2 tk = cscale(cmul(xk, e), wgt);
+            const double2 tn = cscale(cmul(xn, cmul(EN, cconj(e))), wgt);
+            if (two) buf[kn] = tn;  // k = 0: the N slot
+            buf[k] = tk;
+          }
+        }
+      }
+      if (wx)
+        for (int k = NH + lane; k < a.NHP; k += 64) Xr[k] = cmk(0.0, 0.0);
+      pn = wave_sum(pn);
+      pd = wave_sum(pd);
+      if (lane == 0) {
+        const double sig = a.errs ? a.errs[(size_t)s * nchan + n]
+                                  : sqrt(pn / (double)(2 * N) / (double)(NH - a.kc));
+        a.sig[(size_t)c * nchan + n] = sig;
+        a.dsum[(size_t)c * nchan + n] = pd;
+      }
+    } else if (n < nchan) {  // masked channel
+      if (lane == 0) { a.sig[(size_t)c * nchan + n] = 0.0; a.dsum[(size_t)c * nchan + n] = 0.0; }
+      if (wx) {
+        double2* Xr = a.X + ((size_t)c * nchan + n) * a.NHP;
+        for (int k = lane; k < a.NHP; k += 64) Xr[k] = cmk(0.0, 0.0);
       }
     }
-    for (int k = NH + tid; k < a.NHP; k += kBlock) Xr[k] = cmk(0.0, 0.0);
-    pn = wave_sum(pn);
-    pd = wave_sum(pd);
-    double* rd = red[n & 1];
-    if ((tid & 63) == 0) { rd[tid >> 6] = pn; rd[kWaves + (tid >> 6)] = pd; }
-    __syncthreads();  // buf and rd complete; the next row may overwrite buf
-    if (tid == 0) {
-      double sn = 0.0, sd = 0.0;
-      for (int i = 0; i < kWaves; ++i) { sn += rd[i]; sd += rd[kWaves + i]; }
-      const double sig = a.errs ? a.errs[(size_t)s * nchan + n]
-                                : sqrt(sn / (double)(2 * N) / (double)(NH - a.kc));
-      a.sig[(size_t)c * nchan + n] = sig;
-      a.dsum[(size_t)c * nchan + n] = sd;
+    if (a.guess) {
+      __syncthreads();  // the group's rotated rows are complete
+      if constexpr (RREG) {
+#pragma unroll
+        for (int q = 0; q < Cfg::NRQ; ++q) {
+          const int k = tid + nthr * q;
+          if (k <= N)
+#pragma unroll
+            for (int v = 0; v < WPB; ++v)
+              if (s_act[v]) rq[q] = cadd(rq[q], bufs[v][k]);
+        }
+      } else {
+        if (s_act[0])
+          for (int k = tid; k <= N; k += nthr) Rr[k] = cadd(Rr[k], bufs[0][k]);
+      }
+      __syncthreads();  // buffers free for the next group
+    } else {
+      fft_sync<true>();
     }
   }
   if (a.guess) {
-    double2* Rr = a.R + (size_t)c * a.NHP;
-#pragma unroll
-    for (int i = 0; i < KI; ++i) {
-      const int k = tid + i * kBlock;
+    const double iw = 1.0 / wsum;
+    for (int k = tid; k < a.NHP; k += nthr) {
+      double2 r = cmk(0.0, 0.0);
       if (k <= N) {
-        double2 r = cscale(racc[i], 1.0 / wsum);
+        if constexpr (RREG) {
+#pragma unroll
+          for (int q = 0; q < Cfg::NRQ; ++q)
+            if (k == tid + nthr * q) r = rq[q];
+        } else {
+          r = Rr[k];  // accumulated by this same thread
+        }
+        r = cscale(r, iw);
         if (k == 0) r = cmk(0.0, 0.0);
         if (k == N) r.y = 0.0;  // irfft drops Im(X_N)
-        Rr[k] = r;
       }
+      Rr[k] = r;
     }
-    for (int k = NH + tid; k < a.NHP; k += kBlock) Rr[k] = cmk(0.0, 0.0);
   }
 }
 

@@ -134,11 +134,13 @@ class Engine:
                   nu_out=None, errs=None, chan_mask=None, weights=None,
                   model_idx=None, log10_tau=False, option=0, is_toa=True,
                   guess=False, guess_Ns=100, guess_wrap=True, guess_nu=None,
-                  guess_tau=None):
+                  guess_tau=None, exact=False):
         """fit_portrait_full over a batch (pptoaslib.py:928-1096).
 
         data [nsub, nchan, nbin]; model [nmodel, nchan, nbin] (or [nchan, nbin]);
         freqs [nsub, nchan] or [nchan]; P [nsub] or scalar; init [nsub, 5] or [5].
+        exact=True forces the exact cross-spectrum sweeps for phase-family
+        fits (default: per-channel Taylor moments, ppfit_taylor.hip).
         Returns a dict of device tensors.
         """
         dev = self.device
@@ -174,6 +176,7 @@ class Engine:
         desc.guess = int(bool(guess))
         desc.guess_Ns = int(guess_Ns)
         desc.guess_wrap = int(bool(guess_wrap))
+        desc.solver_flags = _lib.PPF_SOLVE_EXACT if exact else 0
         keep = dict(d=d, m=m, fr=fr, P=Pt, it=it, nf=nf, no=no, er=er, mk=mk, wt=wt,
                     mi=mi, gn=gn, gt=gt)
         desc.data, desc.model, desc.model_idx = _ptr(d), _ptr(m), _ptr(mi)
