@@ -83,6 +83,11 @@ int ppf_set_timing(ppf_ctx* ctx, int enable);
 int ppf_get_kernel_time(ppf_ctx* ctx, int kernel_id, double* total_ms,
                         int64_t* launches);
 int ppf_reset_kernel_times(ppf_ctx* ctx);
+/* Device self-test of the cross-lane primitives the kernels rely on
+ * (DPP row/quad moves, permlane16/32 swaps, readlane).  fails[t] (t <
+ * PPF_SELFTEST_N) = number of lanes where test t is wrong; all 0 = pass.   */
+#define PPF_SELFTEST_N 9
+int ppf_selftest(ppf_ctx* ctx, int32_t* fails);
 
 /* ---------------------------------------------------------------------- */
 /* Batched wideband fit: fit_portrait_full over nsub subints.              */

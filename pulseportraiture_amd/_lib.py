@@ -16,6 +16,7 @@ KERNEL_IDS = {"model_fft": 0, "data_xspec": 1, "solve": 2, "phase_shift": 3,
               "rotate": 4, "rot_accum": 5, "synth": 6, "irfft": 7, "noise": 8,
               "guess": 9, "post": 10, "moments": 11}
 PPF_SOLVE_EXACT = 1
+PPF_SELFTEST_N = 9
 
 _dp = ctypes.c_void_p  # device pointers travel as plain addresses
 
@@ -57,6 +58,7 @@ EXPORTS = {
                              ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(ctypes.c_int64)], ctypes.c_int),
     "ppf_reset_kernel_times": ([ctypes.c_void_p], ctypes.c_int),
+    "ppf_selftest": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
     "ppf_fit_portrait_batch": ([ctypes.c_void_p, ctypes.POINTER(FitDesc),
                                 ctypes.POINTER(FitResult)], ctypes.c_int),
     "ppf_phase_shift_batch": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,

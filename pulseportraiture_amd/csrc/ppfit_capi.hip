@@ -429,7 +429,7 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   fa.o_fun = o->fun;
   fa.o_cov_nosc = o->cov_nosc;
 
-  const size_t lds_meta = align256((size_t)nchan * (3 * sizeof(double) + sizeof(int)));
+  const size_t lds_meta = align256((size_t)nchan * (5 * sizeof(double) + sizeof(int)));
   const size_t lds_guess = (size_t)NHP * sizeof(double2);
   for (int64_t s0 = 0; s0 < d->nsub; s0 += chunk) {
     const int nc = (int)std::min<int64_t>(chunk, d->nsub - s0);
@@ -488,6 +488,22 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
         }))
       return r;
   }
+  return PPF_OK;
+}
+
+int ppf_selftest(ppf_ctx* ctx, int32_t* fails) {
+  if (!ctx || !fails) return fail(ctx, PPF_ERR_INVALID, "null argument");
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  int* d = nullptr;
+  HIPCHK(ctx, hipMalloc(&d, PPF_SELFTEST_N * sizeof(int)));
+  (void)hipMemsetAsync(d, 0, PPF_SELFTEST_N * sizeof(int), ctx->stream);
+  hipLaunchKernelGGL(k_selftest, dim3(1), dim3(64), 0, ctx->stream, d);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(fails, d, PPF_SELFTEST_N * sizeof(int), hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(ctx, PPF_ERR_DEVICE, "selftest: %s", hipGetErrorString(e));
   return PPF_OK;
 }
 

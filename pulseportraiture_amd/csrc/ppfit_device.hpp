@@ -56,18 +56,81 @@ __device__ __forceinline__ double2 turn_phasor(double k, double phi) {
   return cmk(c, s);
 }
 
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+// Cross-lane moves without the LDS crossbar: DPP within 16-lane rows and
+// v_permlane16/32_swap across rows (gfx950), each on the two dwords of a double.
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov(double v) {
+  const unsigned long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+// value of the lane in the other 16-lane row of the pair (O = 16) / other half-wave (O = 32)
+template <int O>
+__device__ __forceinline__ double swap_rows(double v) {
+  const unsigned long long u = __double_as_longlong(v);
+  unsigned lo = (unsigned)u, hi = (unsigned)(u >> 32);
+  if constexpr (O == 16) {
+    const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    // lanes of even rows receive in [1], odd rows in [0]
+    const bool odd = (threadIdx.x & 16) != 0;
+    lo = odd ? a[0] : a[1];
+    hi = odd ? b[0] : b[1];
+  } else {
+    const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    const bool up = (threadIdx.x & 32) != 0;
+    lo = up ? a[0] : a[1];
+    hi = up ? b[0] : b[1];
+  }
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// Sum over the 8 lanes that share (lane >> 3): quad xor 1, xor 2, then the
+// half-row mirror pairs the two quads.  Every lane of the 8 gets the sum.
+__device__ __forceinline__ double group8_sum(double v) {
+  v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141>(v);  // row_half_mirror
   return v;
 }
 
-// Sum over the 8 lanes that share (lane >> 3): xor 1, 2, 4.
-__device__ __forceinline__ double group8_sum(double v) {
-  v += __shfl_xor(v, 1);
-  v += __shfl_xor(v, 2);
-  v += __shfl_xor(v, 4);
+// Sum over the wave; every lane gets it.
+__device__ __forceinline__ double wave_sum(double v) {
+  v = group8_sum(v);
+  v += dpp_mov<0x140>(v);  // row_mirror: the two 8-lane halves of a row
+  v += swap_rows<16>(v);
+  v += swap_rows<32>(v);
   return v;
+}
+
+// Max over the wave; every lane gets it.
+__device__ __forceinline__ double wave_max(double v) {
+  v = fmax(v, dpp_mov<0xB1>(v));
+  v = fmax(v, dpp_mov<0x4E>(v));
+  v = fmax(v, dpp_mov<0x141>(v));
+  v = fmax(v, dpp_mov<0x140>(v));
+  v = fmax(v, swap_rows<16>(v));
+  v = fmax(v, swap_rows<32>(v));
+  return v;
+}
+
+// Lane 0's value as a wave-uniform (scalar) double.
+__device__ __forceinline__ double lane0(double v) {
+  const unsigned long long u = __double_as_longlong(v);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// Lane J's value, wave-uniform.
+template <int J>
+__device__ __forceinline__ double lane_at(double v) {
+  const unsigned long long u = __double_as_longlong(v);
+  const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, J);
+  const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), J);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
 // Block-wide sum; `red` is >= kWaves doubles of LDS.  Every thread gets it.

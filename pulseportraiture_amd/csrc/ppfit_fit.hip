@@ -41,20 +41,25 @@ struct Meta {
   double* fr;   // frequency
   double* iw2;  // 1 / errs_FT^2, errs_FT = sigma sqrt(nbin/2) (pptoaslib.py:980-984)
   double* pn;   // sum_{k>=1} |M_nk|^2 (Sbp with tau = 0)
+  double* d1;   // d phi_n / d DM at the subint's nu_fit  (pptoaslib.py:216-225)
+  double* d2;   // d phi_n / d GM at the subint's nu_fit
   int nok;
 };
 
 __device__ __forceinline__ size_t meta_bytes(int nchan) {
-  return (size_t)nchan * (3 * sizeof(double) + sizeof(int));
+  return (size_t)nchan * (5 * sizeof(double) + sizeof(int));
 }
 
+// refs = the subint's nu_fit (SolveState.refs, set by k_guess)
 __device__ Meta load_meta(const FitArgs& a, int c, int s, unsigned char* dyn, int* s_nok) {
   Meta m;
   const int nchan = a.nchan;
   m.fr = reinterpret_cast<double*>(dyn);
   m.iw2 = m.fr + nchan;
   m.pn = m.iw2 + nchan;
-  m.chan = reinterpret_cast<int*>(m.pn + nchan);
+  m.d1 = m.pn + nchan;
+  m.d2 = m.d1 + nchan;
+  m.chan = reinterpret_cast<int*>(m.d2 + nchan);
   const int tid = threadIdx.x, lane = tid & 63;
   const uint8_t* mask = a.mask ? a.mask + (size_t)s * nchan : nullptr;
   if (tid < 64) {
@@ -73,12 +78,20 @@ __device__ Meta load_meta(const FitArgs& a, int c, int s, unsigned char* dyn, in
   m.nok = *s_nok;
   const int midx = a.model_idx ? a.model_idx[s] : 0;
   const double half = 0.5 * (double)a.nbin;
+  const double P = a.P[s];
+  const double* refs = a.st[c].refs;
+  const double r0 = 1.0 / (refs[0] * refs[0]);
+  const double r1 = 1.0 / (refs[1] * refs[1]);
   for (int j = tid; j < m.nok; j += kBlock) {
     const int n = m.chan[j];
-    m.fr[j] = a.freqs[(size_t)s * nchan + n];
+    const double fr = a.freqs[(size_t)s * nchan + n];
+    m.fr[j] = fr;
     const double sg = a.sig[(size_t)c * nchan + n];
     m.iw2[j] = 1.0 / (sg * sg * half);
     m.pn[j] = a.pn[(size_t)midx * nchan + n];
+    const double f2 = 1.0 / (fr * fr);
+    m.d1[j] = kDconst * (f2 - r0) / P;
+    m.d2[j] = kDconst2 * (f2 * f2 - r1 * r1) / P;
   }
   __syncthreads();
   return m;
@@ -242,7 +255,8 @@ struct ChanDeriv {
 template <bool SCAT>
 __device__ __forceinline__ ChanDeriv derive(const double* acc, bool scat, double pn, double iw2,
                                             double fr, const double* prm, double tau_lin,
-                                            const double* refs, double P, bool log10_tau) {
+                                            const double* refs, double P, bool log10_tau,
+                                            const double* dpre = nullptr) {
   ChanDeriv d;
   d.C = acc[0] * iw2;
   d.C1 = -kTwoPi * acc[1] * iw2;
@@ -259,12 +273,17 @@ __device__ __forceinline__ ChanDeriv derive(const double* acc, bool scat, double
     d.F1 = d.F1p = d.G1 = d.SF = d.SFF = d.SG = 0.0;
     d.S = pn * iw2;
   }
-  const double f2 = 1.0 / (fr * fr), f4 = f2 * f2;
-  const double r0 = 1.0 / (refs[0] * refs[0]);
-  const double r1 = 1.0 / (refs[1] * refs[1]);
   d.dph[0] = 1.0;
-  d.dph[1] = kDconst * (f2 - r0) / P;
-  d.dph[2] = kDconst2 * (f4 - r1 * r1) / P;
+  if (dpre) {  // refs = nu_fit: precomputed in Meta
+    d.dph[1] = dpre[0];
+    d.dph[2] = dpre[1];
+  } else {
+    const double f2 = 1.0 / (fr * fr), f4 = f2 * f2;
+    const double r0 = 1.0 / (refs[0] * refs[0]);
+    const double r1 = 1.0 / (refs[1] * refs[1]);
+    d.dph[1] = kDconst * (f2 - r0) / P;
+    d.dph[2] = kDconst2 * (f4 - r1 * r1) / P;
+  }
   if (!SCAT) {
     d.dts[0] = d.dts[1] = 0.0;
     d.d2ts[0] = d.d2ts[1] = d.d2ts[2] = 0.0;
@@ -363,7 +382,16 @@ struct TaylorSrc {
   const int* cnt;      // [nchan] moments stored per row
   const double* xc;    // centre params
   const double* refc;  // centre reference frequencies
+  bool same = false;   // evaluation refs == refc: offsets from Meta d1/d2
 };
+
+// offset from the centre for evaluation refs == centre refs:
+// delta_n = dphi + dDM d1_n + dGM d2_n
+__device__ __forceinline__ double taylor_delta_lin(const double* prm, const double* xc, double d1,
+                                                   double d2) {
+  const double d = fma(prm[2] - xc[2], d2, fma(prm[1] - xc[1], d1, prm[0] - xc[0]));
+  return d - rint(d);
+}
 
 // offset of phi_n(prm, refs) from the centre's phi_n, reduced to [-1/2, 1/2]
 __device__ __forceinline__ double taylor_delta(const double* prm, const double* refs,
@@ -414,9 +442,9 @@ __device__ double taylor_reach(const Meta& m, const double* prm, const double* r
                                const TaylorSrc& ts, double P, double Ks, double* red) {
   double mx = 0.0;
   for (int j = threadIdx.x; j < m.nok; j += kBlock)
-    mx = fmax(mx, fabs(taylor_delta(prm, refs, ts, m.fr[j], P)));
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
+    mx = fmax(mx, fabs(ts.same ? taylor_delta_lin(prm, ts.xc, m.d1[j], m.d2[j])
+                               : taylor_delta(prm, refs, ts, m.fr[j], P)));
+  mx = wave_max(mx);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (lane == 0) red[w] = mx;
   __syncthreads();
@@ -457,8 +485,9 @@ __device__ void sweep(const FitArgs& a, const Meta& m, int c, int s, const doubl
     const double fr = m.fr[jj];
     double acc[NACC];
     if (!SCAT && ts.T) {
-      taylor_cells(ts.T + (size_t)n * kMT, ts.cnt[n], h, taylor_delta(prm, refs, ts, fr, P),
-                   0.5 * (double)a.nbin, acc);
+      const double dl = ts.same ? taylor_delta_lin(prm, ts.xc, m.d1[jj], m.d2[jj])
+                                : taylor_delta(prm, refs, ts, fr, P);
+      taylor_cells(ts.T + (size_t)n * kMT, ts.cnt[n], h, dl, 0.5 * (double)a.nbin, acc);
     } else if (!scat) {
       const double phif = phase_frac(prm, fr, refs, P);
       const double2* Xr = a.X + ((size_t)c * a.nchan + n) * a.NHP;
@@ -476,8 +505,9 @@ __device__ void sweep(const FitArgs& a, const Meta& m, int c, int s, const doubl
 #pragma unroll
     for (int i = 0; i < NP; ++i) ct[i] = 0.0;
     if (h == 0 && valid) {
+      const double dpre[2] = {m.d1[j], m.d2[j]};
       const ChanDeriv d = derive<SCAT>(acc, scat, m.pn[j], m.iw2[j], fr, prm, tau_lin, refs, P,
-                                       log10_tau);
+                                       log10_tau, MODE == 0 ? dpre : nullptr);
       const double q = d.C * d.C / d.S;
       if (MODE == 0) {
         double* dst = acc_slot + (size_t)j * NACC;
@@ -515,10 +545,7 @@ __device__ void sweep(const FitArgs& a, const Meta& m, int c, int s, const doubl
     }
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
-      double v = ct[i];
-      v += __shfl_xor(v, 8);
-      v += __shfl_xor(v, 16);
-      v += __shfl_xor(v, 32);
+      const double v = wave_sum(ct[i]);  // only h == 0 lanes hold terms
       if (lane == 0) red[w][i] += v;
     }
   }
@@ -653,16 +680,15 @@ __global__ void k_model_mean(const double2* __restrict__ M, double2* __restrict_
 // Every lane then runs the same scalar control flow, so the step needs a few
 // registers per lane instead of dozens of 5-vectors on one thread.
 __device__ __forceinline__ double dot8(double a, double b) {
-  double v = a * b;
-  v += __shfl_xor(v, 1);
-  v += __shfl_xor(v, 2);
-  v += __shfl_xor(v, 4);
-  return __shfl(v, 0);
+  return lane0(group8_sum(a * b));
 }
 __device__ __forceinline__ double hvec(const double (&Hrow)[5], double v) {
   double s = 0.0;
-#pragma unroll
-  for (int j = 0; j < 5; ++j) s += Hrow[j] * __shfl(v, j);
+  s += Hrow[0] * lane_at<0>(v);
+  s += Hrow[1] * lane_at<1>(v);
+  s += Hrow[2] * lane_at<2>(v);
+  s += Hrow[3] * lane_at<3>(v);
+  s += Hrow[4] * lane_at<4>(v);
   return s;
 }
 // m(p) = f + g.p + 0.5 p.(H p)   (BaseQuadraticSubproblem.__call__)

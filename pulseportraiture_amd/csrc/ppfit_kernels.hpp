@@ -257,6 +257,7 @@ __global__ void k_guess(FitArgs a);
 __global__ void k_model_mean(const double2* M, double2* Mmean, int nchan, int NHP);
 template <int LOGN> __global__ void k_moments(FitArgs a);
 __global__ void k_solve_taylor(FitArgs a);
+__global__ void k_selftest(int* fails);
 template <bool SCAT> __global__ void k_solve(FitArgs a);
 template <bool SCAT> __global__ void k_post(FitArgs a);
 

@@ -24,7 +24,8 @@
 namespace ppf {
 
 // Reduce 2*NH values per lane over a wave so that, afterwards, each lane
-// holds NH of them summed over the lanes that differ from it in bit `o`.
+// holds NH of them summed over the lanes that differ from it in bit `o`
+// (lanes with that bit set keep the upper half).
 template <int NH>
 __device__ __forceinline__ void rs_step(const double* v, double* out, int o, bool upper) {
 #pragma unroll
@@ -33,6 +34,33 @@ __device__ __forceinline__ void rs_step(const double* v, double* out, int o, boo
     const double send = upper ? v[i] : v[NH + i];
     out[i] = keep + __shfl_xor(send, o);
   }
+}
+
+// The same step for o = 32 / 16 with v_permlane32_swap / v_permlane16_swap:
+// swapping the upper half-wave (odd 16-lane rows) of `lo` with the lower half
+// (even rows) of `hi` leaves lo + hi = the pair sum of the half each lane
+// keeps, with no lane select and no LDS-routed shuffle.
+template <int O>
+__device__ __forceinline__ double pair_swap_sum(double lo, double hi) {
+  const unsigned long long a = __double_as_longlong(lo), b = __double_as_longlong(hi);
+  unsigned a0 = (unsigned)a, a1 = (unsigned)(a >> 32), b0 = (unsigned)b, b1 = (unsigned)(b >> 32);
+  if constexpr (O == 32) {
+    const auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+    const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+    a0 = r0[0]; b0 = r0[1]; a1 = r1[0]; b1 = r1[1];
+  } else {
+    static_assert(O == 16, "permlane swaps exist for 16 and 32");
+    const auto r0 = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
+    const auto r1 = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
+    a0 = r0[0]; b0 = r0[1]; a1 = r1[0]; b1 = r1[1];
+  }
+  return __longlong_as_double((long long)(((unsigned long long)a1 << 32) | a0)) +
+         __longlong_as_double((long long)(((unsigned long long)b1 << 32) | b0));
+}
+template <int NH, int O>
+__device__ __forceinline__ void rs_swap(const double* v, double* out) {
+#pragma unroll
+  for (int i = 0; i < NH; ++i) out[i] = pair_swap_sum<O>(v[i], v[NH + i]);
 }
 
 // Moment chunks: moments are formed 8 at a time (m in [8c, 8c + 8)); after
@@ -165,8 +193,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_moments(FitArgs a) {
       }
       // 32 -> 16 -> ... -> 1 value per lane pair: lane L holds value L >> 1
       double r16[16], r8[8], r4[4], r2[2], r1[1];
-      rs_step<16>(acc, r16, 32, (lane & 32) != 0);
-      rs_step<8>(r16, r8, 16, (lane & 16) != 0);
+      rs_swap<16, 32>(acc, r16);
+      rs_swap<8, 16>(r16, r8);
       rs_step<4>(r8, r4, 8, (lane & 8) != 0);
       rs_step<2>(r4, r2, 4, (lane & 4) != 0);
       rs_step<1>(r2, r1, 2, (lane & 2) != 0);
@@ -203,8 +231,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_moments(FitArgs a) {
         }
         // 16 -> 8 -> 4 -> 2 -> 1 values per lane, then lane bits 1, 0
         double r8[8], r4[4], r2[2], r1[1];
-        rs_step<8>(acc, r8, 32, (lane & 32) != 0);
-        rs_step<4>(r8, r4, 16, (lane & 16) != 0);
+        rs_swap<8, 32>(acc, r8);
+        rs_swap<4, 16>(r8, r4);
         rs_step<2>(r4, r2, 8, (lane & 8) != 0);
         rs_step<1>(r2, r1, 4, (lane & 4) != 0);
         r1[0] += __shfl_xor(r1[0], 2);
@@ -247,7 +275,7 @@ __device__ __forceinline__ int pick_centre(const FitArgs& a, const Meta& m, cons
   for (int q = 0; q < 2; ++q) {
     if (!(st.mvalid & (1 << q))) continue;
     const TaylorSrc tq{a.T + ((size_t)c * 2 + q) * a.nchan * kMT,
-                       a.Tcnt + ((size_t)c * 2 + q) * a.nchan, st.xc[q], st.refs};
+                       a.Tcnt + ((size_t)c * 2 + q) * a.nchan, st.xc[q], st.refs, true};
     const double y = taylor_reach(m, prm, refs, tq, P, Ks, red);
     if (y <= kTaylorY && y < by) { by = y; best = q; ts = tq; }
   }
@@ -396,6 +424,28 @@ __global__ __launch_bounds__(kBlock) void k_solve_taylor(FitArgs a) {
     st.fin = 1;
     st.scat_post = false;
   }
+}
+
+// ---------------------------------------------------------------------------
+// Device self-test of the cross-lane primitives (DPP, permlane swaps,
+// readlane) whose lane semantics the reductions above rely on.
+// fails[t] counts the lanes where test t disagrees with its definition.
+// ---------------------------------------------------------------------------
+__global__ void k_selftest(int* fails) {
+  const int l = threadIdx.x & 63;
+  const double x = (double)l;
+  auto chk = [&](int t, bool ok) { if (!ok) atomicAdd(&fails[t], 1); };
+  chk(0, wave_sum(x) == 2016.0);
+  chk(1, group8_sum(x) == (double)(8 * (l & ~7) + 28));
+  chk(2, swap_rows<16>(x) == (double)(l ^ 16));
+  chk(3, swap_rows<32>(x) == (double)(l ^ 32));
+  chk(4, pair_swap_sum<32>(x, 100.0 + x) ==
+             (l < 32 ? (double)(2 * l + 32) : 200.0 + (double)(2 * l - 32)));
+  chk(5, pair_swap_sum<16>(x, 100.0 + x) ==
+             ((l & 16) == 0 ? (double)(2 * l + 16) : 200.0 + (double)(2 * l - 16)));
+  chk(6, wave_max(x * (l == 37 ? 2.0 : 1.0)) == 74.0);
+  chk(7, lane0(x + 3.0) == 3.0 && lane_at<4>(x) == 4.0);
+  chk(8, dpp_mov<0xB1>(x) == (double)(l ^ 1) && dpp_mov<0x4E>(x) == (double)(l ^ 2));
 }
 
 #define PPF_INST_TAYLOR(L) template __global__ void k_moments<L>(FitArgs);

@@ -115,6 +115,13 @@ class Engine:
                                                ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value
 
+    def selftest(self):
+        """Device check of the cross-lane primitives (DPP, permlane swaps);
+        returns the per-test failing-lane counts (all 0 = pass)."""
+        fails = (ctypes.c_int32 * _lib.PPF_SELFTEST_N)()
+        self._chk(self.lib.ppf_selftest(self.ctx, fails))
+        return list(fails)
+
     def reset_kernel_times(self):
         self._chk(self.lib.ppf_reset_kernel_times(self.ctx))
 

@@ -25,6 +25,11 @@ def eng():
 NBINS = [64, 128, 256, 512, 1024, 2048, 4096, 8192]
 
 
+def test_cross_lane_selftest(eng):
+    """DPP / permlane16,32 swap / readlane semantics the reductions rely on."""
+    assert eng.selftest() == [0] * 9
+
+
 @pytest.mark.parametrize("nbin", NBINS)
 def test_noise_rows(eng, nbin):
     rng = np.random.default_rng(nbin)
