@@ -64,7 +64,7 @@ extern "C" {
 #define PPF_K_NOISE 8
 #define PPF_K_GUESS 9
 #define PPF_K_POST 10
-#define PPF_K_MOMENTS 11
+#define PPF_K_FIT_TAYLOR 11
 #define PPF_NUM_KERNELS 12
 
 typedef struct ppf_ctx ppf_ctx;
@@ -86,8 +86,16 @@ int ppf_reset_kernel_times(ppf_ctx* ctx);
 /* Device self-test of the cross-lane primitives the kernels rely on
  * (DPP row/quad moves, permlane16/32 swaps, readlane).  fails[t] (t <
  * PPF_SELFTEST_N) = number of lanes where test t is wrong; all 0 = pass.   */
-#define PPF_SELFTEST_N 9
+#define PPF_SELFTEST_N 10
 int ppf_selftest(ppf_ctx* ctx, int32_t* fails);
+/* Diagnostic phase clock of the Taylor fit kernel (off by default).  When
+ * enabled, every k_fit_taylor workgroup adds its wall_clock64 ticks (100 MHz)
+ * per phase into device counters: out[0] guess, [1] meta + first moments,
+ * [2] centre selection incl. recentring, [3] objective sweeps, [4] trust-
+ * region step, [8] recentring passes, [9] workgroups.  The call copies the
+ * counters to out (if non-null), zeroes them and sets the enable state.   */
+#define PPF_PHASE_N 16
+int ppf_phase_profile(ppf_ctx* ctx, int32_t enable, uint64_t* out);
 
 /* ---------------------------------------------------------------------- */
 /* Batched wideband fit: fit_portrait_full over nsub subints.              */

@@ -14,9 +14,10 @@ PPF_OK = 0
 PPF_METHOD_TRUST_NCG = 0
 KERNEL_IDS = {"model_fft": 0, "data_xspec": 1, "solve": 2, "phase_shift": 3,
               "rotate": 4, "rot_accum": 5, "synth": 6, "irfft": 7, "noise": 8,
-              "guess": 9, "post": 10, "moments": 11}
+              "guess": 9, "post": 10, "fit_taylor": 11}
 PPF_SOLVE_EXACT = 1
-PPF_SELFTEST_N = 9
+PPF_SELFTEST_N = 10
+PPF_PHASE_N = 16
 
 _dp = ctypes.c_void_p  # device pointers travel as plain addresses
 
@@ -59,6 +60,8 @@ EXPORTS = {
                              ctypes.POINTER(ctypes.c_int64)], ctypes.c_int),
     "ppf_reset_kernel_times": ([ctypes.c_void_p], ctypes.c_int),
     "ppf_selftest": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
+    "ppf_phase_profile": ([ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_uint64)],
+                          ctypes.c_int),
     "ppf_fit_portrait_batch": ([ctypes.c_void_p, ctypes.POINTER(FitDesc),
                                 ctypes.POINTER(FitResult)], ctypes.c_int),
     "ppf_phase_shift_batch": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,

@@ -35,10 +35,12 @@ struct ppf_ctx {
   std::string err;
   int64_t ws_limit = (int64_t)32 << 30;
   double2* tw[16] = {nullptr};
-  Buffer ws;      // per-chunk fit workspace
+  Buffer ws;     // per-chunk fit workspace
   Buffer mspec;   // template spectra
   Buffer aux;     // misc (synth templates, partial sums)
   Buffer mmean;   // mean template spectra (guess)
+  Buffer ptime;   // k_fit_taylor phase clocks (ppf_phase_profile)
+  bool phase_prof = false;
   bool timing = false;
   std::vector<TimedLaunch> pending;
   std::vector<hipEvent_t> pool;
@@ -293,22 +295,10 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   if (int r = model_spectra(ctx, d->nmodel * nchan, nbin, d->model, 1, ctx->mspec, &M, &pn))
     return r;
 
-  // X (the exact cross-spectrum) is needed only when some subint is fitted
-  // with scattering (or when exact sweeps are forced); phase-family subints
-  // keep kMT Taylor moments per channel instead.
+  // X, the cross-spectrum, is written once by k_data_xspec.  Phase-family
+  // subints are fitted from Taylor moments of it (k_fit_taylor); scattering
+  // fits, and every fit under PPF_SOLVE_EXACT, sweep it directly.
   const bool exact = (d->solver_flags & PPF_SOLVE_EXACT) != 0;
-  bool need_x = exact || d->fit_flags[3] || d->fit_flags[4];
-  if (!need_x) {
-    std::vector<double> hinit((size_t)d->nsub * 5);
-    HIPCHK(ctx, hipMemcpyAsync(hinit.data(), d->init, hinit.size() * sizeof(double),
-                               hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-    for (int64_t i = 0; i < d->nsub && !need_x; ++i) {
-      const double t3 = hinit[(size_t)i * 5 + 3];
-      const double tl = d->log10_tau ? std::pow(10.0, t3) : t3;
-      need_x = tl != 0.0;
-    }
-  }
   const bool taylor = !exact;
   // mean template spectrum for the unmasked guess
   double2* Mmean = nullptr;
@@ -323,13 +313,13 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   }
 
   // per-subint workspace layout
-  const size_t bX = need_x ? (size_t)nchan * NHP * sizeof(double2) : 0;
+  const size_t bX = (size_t)nchan * NHP * sizeof(double2);
   const size_t bT = taylor ? (size_t)2 * nchan * (kMT * sizeof(double2) + sizeof(int)) : 0;
   const size_t bR = (size_t)NHP * sizeof(double2);
   const size_t bC = (size_t)nchan * sizeof(double);
   const size_t bAcc = (size_t)2 * nchan * 10 * sizeof(double);
   const size_t bW = (size_t)nchan * 8 * sizeof(double);
-  const size_t per_sub = bX + bT + 2 * bR + 2 * bC + sizeof(SolveState) + bAcc + bW + sizeof(int);
+  const size_t per_sub = bX + bT + 2 * bR + 2 * bC + sizeof(SolveState) + bAcc + bW;
   int64_t chunk = ctx->ws_limit / (int64_t)(per_sub + 1024);
   if (chunk < 1) chunk = 1;
   if (chunk > d->nsub) chunk = d->nsub;
@@ -343,9 +333,7 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   const size_t offAcc = align256(offSt + cs * sizeof(SolveState));
   const size_t offW = align256(offAcc + cs * bAcc);
   const size_t offT = align256(offW + cs * bW);
-  const size_t offL = align256(offT + cs * bT);
-  const size_t offN = align256(offL + cs * sizeof(int));
-  const size_t total = align256(offN + sizeof(int));
+  const size_t total = align256(offT + cs * bT);
   if (int r = ensure(ctx, ctx->ws, total)) return r;
   char* base = static_cast<char*>(ctx->ws.p);
 
@@ -367,7 +355,7 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   sa.log10_tau = d->log10_tau;
   sa.fit_tau = d->fit_flags[3] ? 1 : 0;
   sa.exact = exact ? 1 : 0;
-  sa.X = need_x ? reinterpret_cast<double2*>(base + offX) : nullptr;
+  sa.X = reinterpret_cast<double2*>(base + offX);
   sa.R = reinterpret_cast<double2*>(base + offR);
   sa.sig = reinterpret_cast<double*>(base + offSig);
   sa.dsum = reinterpret_cast<double*>(base + offDs);
@@ -407,12 +395,9 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   fa.T = taylor ? reinterpret_cast<double2*>(base + offT) : nullptr;
   fa.Tcnt = taylor ? reinterpret_cast<int*>(base + offT + cs * 2 * nchan * kMT * sizeof(double2))
                    : nullptr;
-  fa.data = d->data;
   fa.tw = tw;
   fa.Mmean = Mmean;
-  fa.rq_list = nullptr;
-  fa.rq_count = reinterpret_cast<int*>(base + offN);
-  int* rq_list = reinterpret_cast<int*>(base + offL);
+  fa.ptime = ctx->phase_prof ? static_cast<unsigned long long*>(ctx->ptime.p) : nullptr;
   fa.o_params = o->params;
   fa.o_param_errs = o->param_errs;
   fa.o_nu_out = o->nu_out;
@@ -445,42 +430,20 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
                              ctx->stream, fa);
         }))
       return r;
-    // each subint runs in exactly one of the phase-only / scattering /
-    // Taylor variants (the others exit at once)
+    // each subint runs in exactly one of the exact phase-only / scattering /
+    // fused Taylor variants (the others exit at once)
     if (int r = timed(ctx, PPF_K_SOLVE, [&] {
-          if (!taylor)
+          if (exact)
             hipLaunchKernelGGL(k_solve<false>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
-          if (need_x)
-            hipLaunchKernelGGL(k_solve<true>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
+          hipLaunchKernelGGL(k_solve<true>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
         }))
       return r;
     if (taylor) {
-      FitArgs ma = fa;
-      int nlist = nc;
-      for (int round = 0;; ++round) {
-        if (round > 4000) return fail(ctx, PPF_ERR_DEVICE, "Taylor recentring did not settle");
-        if (int r = timed(ctx, PPF_K_MOMENTS, [&] {
-              LOGN_SWITCH(logN, hipLaunchKernelGGL(k_moments<LG>, dim3(nlist),
-                                                   dim3(MomentsCfg<LG>::WPB * 64), 0, ctx->stream,
-                                                   ma));
-            }))
-          return r;
-        HIPCHK(ctx, hipMemsetAsync(fa.rq_count, 0, sizeof(int), ctx->stream));
-        fa.rq_list = rq_list;
-        if (int r = timed(ctx, PPF_K_SOLVE, [&] {
-              hipLaunchKernelGGL(k_solve_taylor, dim3(nc), dim3(kBlock), lds_meta, ctx->stream,
-                                 fa);
-            }))
-          return r;
-        fa.rq_list = nullptr;
-        int hcount = 0;
-        HIPCHK(ctx, hipMemcpyAsync(&hcount, fa.rq_count, sizeof(int), hipMemcpyDeviceToHost,
-                                   ctx->stream));
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-        if (hcount == 0) break;
-        ma.rq_list = rq_list;
-        nlist = hcount;
-      }
+      if (int r = timed(ctx, PPF_K_FIT_TAYLOR, [&] {
+            hipLaunchKernelGGL(k_fit_taylor, dim3(nc), dim3(kBlock), lds_meta + lds_guess,
+                               ctx->stream, fa);
+          }))
+        return r;
     }
     if (int r = timed(ctx, PPF_K_POST, [&] {
           hipLaunchKernelGGL(k_post<false>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
@@ -488,6 +451,21 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
         }))
       return r;
   }
+  return PPF_OK;
+}
+
+int ppf_phase_profile(ppf_ctx* ctx, int32_t enable, uint64_t* out) {
+  if (!ctx) return fail(ctx, PPF_ERR_INVALID, "null context");
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  const size_t bytes = PPF_PHASE_N * sizeof(uint64_t);
+  if (!ctx->ptime.p) {
+    if (int r = ensure(ctx, ctx->ptime, bytes)) return r;
+    HIPCHK(ctx, hipMemsetAsync(ctx->ptime.p, 0, bytes, ctx->stream));
+  }
+  if (out) HIPCHK(ctx, hipMemcpyAsync(out, ctx->ptime.p, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, hipMemsetAsync(ctx->ptime.p, 0, bytes, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->phase_prof = enable != 0;
   return PPF_OK;
 }
 

@@ -454,6 +454,81 @@ __device__ double taylor_reach(const Meta& m, const double* prm, const double* r
   return kTwoPi * Ks * r;
 }
 
+// Solver sweep of a phase-family fit from Taylor moments (refs = nu_fit, so
+// d phi_n / d(DM, GM) are Meta's d1, d2).  With tau = 0, S_n = p_n / errs^2
+// does not depend on the parameters and every term of pptoaslib.py:525-643
+// factors into a per-channel scalar times products of dphi_n:
+//   f  = sum -C^2/S,  g_i = sum gc dph_i,  H_ij = sum hc dph_i dph_j,
+//   gc = -2 C C1 / S,  hc = -2 (C C2 + C1^2) / S,
+// so each lane carries 10 running sums over its channel groups and the wave
+// reduces them once, instead of 21 reductions per group.
+__device__ void sweep_taylor0(const FitArgs& a, const Meta& m, const double* prm,
+                              double* acc_slot, double* out, double (*red)[48],
+                              const TaylorSrc& ts) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g8 = lane >> 3, h = lane & 7;
+  const double Ks = 0.5 * (double)a.nbin;
+  double t[10];
+#pragma unroll
+  for (int i = 0; i < 10; ++i) t[i] = 0.0;
+  const int ngroups = (m.nok + 7) >> 3;
+  for (int gi = w; gi < ngroups; gi += kWaves) {
+    const int j = gi * 8 + g8;
+    const bool valid = j < m.nok;
+    const int jj = valid ? j : m.nok - 1;
+    const int n = m.chan[jj];
+    const double d1 = m.d1[jj], d2 = m.d2[jj];
+    double acc[NACC];
+    taylor_cells(ts.T + (size_t)n * kMT, ts.cnt[n], h, taylor_delta_lin(prm, ts.xc, d1, d2), Ks,
+                 acc);
+    const double s0 = group8_sum(acc[0]), s1 = group8_sum(acc[1]), s2 = group8_sum(acc[2]);
+    if (h == 0 && valid) {
+      double* dst = acc_slot + (size_t)j * NACC;
+      dst[0] = s0;
+      dst[1] = s1;
+      dst[2] = s2;
+      const double iw2 = m.iw2[j];
+      const double C = s0 * iw2, C1 = -kTwoPi * s1 * iw2, C2 = -kFourPi2 * s2 * iw2;
+      const double iS = 1.0 / (m.pn[j] * iw2);
+      const double gc = -2.0 * C * C1 * iS;
+      const double hc = -2.0 * (C * C2 + C1 * C1) * iS;
+      t[0] -= C * C * iS;
+      t[1] += gc;
+      t[2] = fma(gc, d1, t[2]);
+      t[3] = fma(gc, d2, t[3]);
+      t[4] += hc;
+      t[5] = fma(hc, d1, t[5]);
+      t[6] = fma(hc, d2, t[6]);
+      t[7] = fma(hc * d1, d1, t[7]);
+      t[8] = fma(hc * d1, d2, t[8]);
+      t[9] = fma(hc * d2, d2, t[9]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const double v = wave_sum(t[i]);
+    if (lane == 0) red[w][i] = v;
+  }
+  __syncthreads();
+  if (tid < 21) {
+    // out[0] f, out[1..5] g, out[6 + p] H pair p: (0,0) 0, (0,1) 1, (0,2) 2,
+    // (1,1) 5, (1,2) 6, (2,2) 9; tau/alpha entries are 0
+    int src = -1;
+    bool on = true;
+    if (tid == 0) src = 0;
+    else if (tid < 4) { src = tid; on = a.flags[tid - 1]; }
+    else if (tid >= 6) {
+      const int p = tid - 6, pi = pair_i(p), pj = pair_j(p);
+      if (pj < 3) { src = 4 + (pi == 0 ? pj : 1 + pi + pj); on = a.flags[pi] && a.flags[pj]; }
+    }
+    double v = 0.0;
+    if (src >= 0 && on)
+      for (int q = 0; q < kWaves; ++q) v += red[q][src];
+    out[tid] = v;
+  }
+  __syncthreads();
+}
+
 // One sweep over all fitted channels at (prm, refs).  MODE 0: f, g, H for
 // the solver (out[0..20]) and raw accumulators into acc_slot; MODE 1: the
 // with-scales Hessian pieces (out[0..29]) and per-channel wsc rows.  SCAT
@@ -466,6 +541,12 @@ template <int MODE, bool SCAT>
 __device__ void sweep(const FitArgs& a, const Meta& m, int c, int s, const double* prm,
                       const double* refs, double P, double* acc_slot, double* out,
                       double (*red)[48], const TaylorSrc& ts) {
+  if constexpr (MODE == 0 && !SCAT) {
+    if (ts.T && ts.same) {
+      sweep_taylor0(a, m, prm, acc_slot, out, red, ts);
+      return;
+    }
+  }
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g8 = lane >> 3, h = lane & 7;
   const int J = a.NHP >> 3;
@@ -561,11 +642,19 @@ __device__ void sweep(const FitArgs& a, const Meta& m, int c, int s, const doubl
 // ---------------------------------------------------------------------------
 // k_guess
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_guess(FitArgs a) {
-  extern __shared__ __align__(16) unsigned char dyn[];
-  __shared__ GuessShared gs;
-  __shared__ double s_v[4];
-  const int c = blockIdx.x, s = a.sub0 + c, tid = threadIdx.x;
+// Subints whose fit runs in k_fit_taylor (ppfit_taylor.hip): phase family
+// (tau = 0 at the start and not fitted) when the Taylor path is on.
+__device__ __forceinline__ bool fused_taylor(const FitArgs& a, int s) {
+  if (!a.T) return false;
+  const double t3 = a.init[(size_t)s * 5 + 3];
+  const double tl = a.log10_tau ? pow(10.0, t3) : t3;
+  return !((tl != 0.0) || a.flags[3]);
+}
+
+// Solver-state set-up and the get_TOAs initial phase of one subint (all
+// threads of the block).  dyn: >= NHP double2 of LDS for the guess spectrum.
+__device__ void guess_subint(const FitArgs& a, int c, int s, unsigned char* dyn, GuessShared& gs) {
+  const int tid = threadIdx.x;
   const int nchan = a.nchan;
   const uint8_t* mask = a.mask ? a.mask + (size_t)s * nchan : nullptr;
   double fsum = 0.0, cnt = 0.0;
@@ -653,7 +742,21 @@ __global__ __launch_bounds__(kBlock) void k_guess(FitArgs a) {
     st.x[0] = phi;
     for (int i = 0; i < 5; ++i) { st.init[i] = st.x[i]; st.xc[0][i] = st.x[i]; }
   }
-  (void)s_v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_guess(FitArgs a) {
+  extern __shared__ __align__(16) unsigned char dyn[];
+  __shared__ GuessShared gs;
+  const int c = blockIdx.x, s = a.sub0 + c;
+  if (fused_taylor(a, s)) {  // k_fit_taylor owns this subint: keep the
+    if (threadIdx.x == 0) {  // exact-path kernels launched around it off it
+      a.st[c].scat = 0;
+      a.st[c].scat_post = 0;
+      a.st[c].taylor = 1;
+    }
+    return;
+  }
+  guess_subint(a, c, s, dyn, gs);
 }
 
 // Mean of the DC-zeroed channel spectra of each template (unmasked guess
@@ -1111,12 +1214,11 @@ struct PostShared {
   double fmean, Sd;
 };
 
+// zero-covariance frequencies, outputs at nu_out and the with-scales
+// covariance of one subint (all threads of the block)
 template <bool SCAT>
-__global__ __launch_bounds__(kBlock) void k_post(FitArgs a) {
-  extern __shared__ __align__(16) unsigned char dyn[];
-  __shared__ PostShared sh;
-  const int c = blockIdx.x, s = a.sub0 + c, tid = threadIdx.x;
-  if ((a.st[c].scat_post != 0) != SCAT) return;
+__device__ void post_subint(const FitArgs& a, int c, int s, unsigned char* dyn, PostShared& sh) {
+  const int tid = threadIdx.x;
   const int nchan = a.nchan;
   const Meta m = load_meta(a, c, s, dyn, &sh.nok);
   const SolveState& st = a.st[c];
@@ -1323,6 +1425,15 @@ __global__ __launch_bounds__(kBlock) void k_post(FitArgs a) {
     if (a.o_init_used) for (int i = 0; i < 5; ++i) a.o_init_used[(size_t)s * 5 + i] = st.init[i];
     if (a.o_fun) a.o_fun[s] = st.fun;
   }
+}
+
+template <bool SCAT>
+__global__ __launch_bounds__(kBlock) void k_post(FitArgs a) {
+  extern __shared__ __align__(16) unsigned char dyn[];
+  __shared__ PostShared sh;
+  const int c = blockIdx.x, s = a.sub0 + c;
+  if ((a.st[c].scat_post != 0) != SCAT) return;
+  post_subint<SCAT>(a, c, s, dyn, sh);
 }
 
 }  // namespace ppf

@@ -84,11 +84,9 @@ struct FitArgs {
   SolveState* st;            // chunk [c]
   double2* T;                // chunk [c][2][nchan][kMT] Taylor moments
   int* Tcnt;                 // chunk [c][2][nchan] moments stored per row
-  const double* data;        // [nsub][nchan][nbin] (k_moments)
   const double2* tw;         // rfft twiddles e^{-2 pi i m / nbin}
   const double2* Mmean;      // [nmodel][NHP] mean template spectrum or null
-  int* rq_list;              // chunk: subints waiting for a recentre
-  int* rq_count;
+  unsigned long long* ptime; // [PPF_PHASE_N] k_fit_taylor phase clocks, or null
   double* acc;               // chunk [c][2][nchan][10]
   double* wsc;               // chunk [c][nchan][8]
   // outputs (global batch index sub0 + c)
@@ -255,8 +253,7 @@ __global__ void k_rot_accum(const double* data, const double* phase, const doubl
 __global__ void k_accum_reduce(const double2* partial, double2* accum, int nsplit, size_t count);
 __global__ void k_guess(FitArgs a);
 __global__ void k_model_mean(const double2* M, double2* Mmean, int nchan, int NHP);
-template <int LOGN> __global__ void k_moments(FitArgs a);
-__global__ void k_solve_taylor(FitArgs a);
+__global__ void k_fit_taylor(FitArgs a);
 __global__ void k_selftest(int* fails);
 template <bool SCAT> __global__ void k_solve(FitArgs a);
 template <bool SCAT> __global__ void k_post(FitArgs a);

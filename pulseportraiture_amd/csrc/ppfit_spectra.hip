@@ -141,13 +141,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
   }
   __syncthreads();
   const double wsum = s_meta[1];
-  // X is needed only by the exact (scattering) sweeps
-  bool wx = a.X != nullptr;
-  if (wx && !a.exact) {
-    const double t3 = a.init[(size_t)s * 5 + 3];
-    const double tl = a.log10_tau ? pow(10.0, t3) : t3;
-    wx = (tl != 0.0) || a.fit_tau;
-  }
+  const bool wx = a.X != nullptr;
   {
     const double nug = s_meta[0];
     const double Dfac = kDconst * s_meta[3] / a.P[s];

@@ -63,207 +63,101 @@ __device__ __forceinline__ void rs_swap(const double* v, double* out) {
   for (int i = 0; i < NH; ++i) out[i] = pair_swap_sum<O>(v[i], v[NH + i]);
 }
 
-// Moment chunks: moments are formed 8 at a time (m in [8c, 8c + 8)); after
-// chunk c the row's own absolute moments bound the truncation of a series
-// that stops at Mt = 8c + 6 terms (T up to index Mt + 1 is stored):
-//   |sum_{m >= Mt} (iy)^m/m! T_{m+p}| <= A_Mt e^Y Y^Mt / Mt!,
-//   A_m = sum_k v_k^m (|Re W_k| + |Im W_k|)  (non-increasing in m, v <= 1),
-// and the row stops once that is <= 2^-57 A_2, i.e. below the rounding of the
-// exact sums (which is ~eps sum_k k^p |W_k|, and A_2 <= A_1 <= A_0).  Pulse
-// spectra sit at low harmonics, so most rows stop after 2 chunks instead of
-// the worst case 4.  The count of stored moments goes to Tcnt.
-__device__ __forceinline__ double taylor_tail_factor(int Mt) {
-  // e^3 * 3^Mt / Mt! for Mt = 6, 14, 22, 30 (kTaylorY = 3)
-  switch (Mt) {
-    case 6: return 20.085536923187668 * 729.0 / 720.0;
-    case 14: return 20.085536923187668 * 4782969.0 / 87178291200.0;
-    case 22: return 20.085536923187668 * 31381059609.0 / 1.1240007277776077e21;
-    default: return 20.085536923187668 * 205891132094649.0 / 2.652528598121911e32;
-  }
-}
-
-template <int LOGN>
-struct MomentsCfg {
-  static constexpr int N = 1 << LOGN;
-  static constexpr int WPB = LOGN <= 10 ? 4 : (LOGN == 11 ? 2 : 1);
-  static constexpr int NB = N + 8;
-  static constexpr int NPI = (N / 2 + 1 + 63) / 64;
-};
-
 // ---------------------------------------------------------------------------
-// k_moments: one workgroup per subint (or per listed subint when recentring);
-// wave w transforms channels n = w, w + WPB, ... and writes T[c][wslot][n].
+// Moments of the fitted channels of subint c about centre xc (at refs), from
+// the cross-spectrum rows X written by k_data_xspec, into T[c][slot]:
+//   T_nm = sum_k v_k^m W_nk,  v_k = k / N,  W_nk = X_nk e^{2 pi i k phi_c,n}.
+// The k-contraction runs on the f64 matrix cores: each wave takes tiles of 8
+// fitted channels; per step of 4 harmonics, v_mfma_f64_16x16x4 multiplies
+// A = v^m (16 moments x 4 harmonics) by B = W (4 harmonics x 16 columns =
+// 8 channels x re/im) into two accumulators (moments 0-15, 16-31).  Lane l
+// supplies harmonic 4 s + (l >> 4) of channel (l & 15) >> 1, part l & 1 to B
+// and v^(l & 15), v^(16 + (l & 15)) of that harmonic to A (by squaring; v is
+// exact since N is a power of two).  X rows stream through registers kMomU
+// steps ahead of the MFMAs, so every wave keeps kMomU row loads in flight and
+// the pass runs at HBM rate instead of load latency.  All kMT moments are
+// kept (cnt = kMT): the truncation bound then holds for any spectrum.
 // ---------------------------------------------------------------------------
-template <int LOGN>
-__global__ __launch_bounds__(kBlock, 2) void k_moments(FitArgs a) {
-  using Cfg = MomentsCfg<LOGN>;
-  constexpr int N = Cfg::N;
-  constexpr int WPB = Cfg::WPB;
-  constexpr int NPI = Cfg::NPI;
-  constexpr int NTW = PassTw<LOGN>::SIZE;
-  constexpr int KW = (N + 1 + 63) / 64;   // harmonics per lane (k = lane + 64 i <= N)
-  static_assert(kMT == 32, "moment chunks below assume 4 x 8 moments");
-  __shared__ double2 bufs[WPB][Cfg::NB];
-  __shared__ double2 twl[NTW];
-  const int c = a.rq_list ? a.rq_list[blockIdx.x] : (int)blockIdx.x;
-  const int s = a.sub0 + c;
-  SolveState& st = a.st[c];
-  if (!st.taylor) return;
-  const int slot = st.wslot;
-  const int nchan = a.nchan;
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+constexpr int kMomU = 8;
+
+__device__ void moments_from_X(const FitArgs& a, const Meta& m, int c, int s, int slot,
+                               const double* xc, const double* refs, double P) {
+  static_assert(kMT == 32, "two 16-row MFMA tiles");
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const uint8_t* mask = a.mask ? a.mask + (size_t)s * nchan : nullptr;
-  const double* drow0 = a.data + (size_t)s * nchan * (2 * N);
-  double2* buf = bufs[w];
-  WaveRow<LOGN> row;
-  int n = next_chan(w, WPB, nchan, mask);
-  if (n < nchan) row.load(drow0 + (size_t)n * 2 * N, lane);
-  fill_pass_tw<LOGN>(twl, a.tw, tid, WPB * 64);
-  double xc[5], refs[3];
+  const int nchan = a.nchan;
+  const int N = a.nbin / 2;
+  const double iN = 1.0 / (double)N;
+  const int nblk = ((N + 1 + 3) / 4 + kMomU - 1) / kMomU;  // blocks of kMomU 4-harmonic steps
+  const int col = lane & 15, chl = col >> 1, part = col & 1, kk = lane >> 4;
+  for (int t = w; t * 8 < m.nok; t += kWaves) {
+    const int j = t * 8 + chl;
+    const bool ok = j < m.nok;
+    const int n = ok ? m.chan[j] : 0;
+    const double2* __restrict__ Xr = a.X + ((size_t)c * nchan + n) * a.NHP;
+    const double phic = ok ? phase_frac(xc, m.fr[j], refs, P) : 0.0;
+    const double2 s4 = turn_phasor(4.0, phic);
+    f64x4 d0 = {0.0, 0.0, 0.0, 0.0}, d1 = {0.0, 0.0, 0.0, 0.0};
+    double2 xb[kMomU];
 #pragma unroll
-  for (int i = 0; i < 5; ++i) xc[i] = st.xc[slot][i];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) refs[i] = st.refs[i];
-  const double P = a.P[s];
-  const int midx = a.model_idx ? a.model_idx[s] : 0;
-  const double* fr = a.freqs + (size_t)s * nchan;
-  const double iKs = 1.0 / (double)N;
-  double sw, cw;
-  sincospi(-(double)lane / (double)N, &sw, &cw);
-  const double2 w0 = cmk(cw, sw);
-  double ss, cs;
-  sincospi(-64.0 / (double)N, &ss, &cs);
-  const double2 wstep = cmk(cs, ss);
-  __syncthreads();  // twl
-  while (n < nchan) {
-    row.store(buf, drow0 + (size_t)n * 2 * N, lane);
-    const int nn = next_chan(n + WPB, WPB, nchan, mask);
-    if (nn < nchan) row.load(drow0 + (size_t)nn * 2 * N, lane);
-    fft_sync<true>();
-    wave_fft<LOGN>(buf, twl, lane);
-    // W_k = D_k conj(M_k) e^{2 pi i k phi_c}, written over the packed FFT in
-    // (k, N-k) pairs (each pair's two slots are read and written by one lane)
-    const double phic = phase_frac(xc, fr[n], refs, P);
-    double2 e = turn_phasor((double)lane, phic);
-    const double2 estep = turn_phasor(64.0, phic);
-    const double2 EN = turn_phasor((double)N, phic);
-    const double2* Mr = a.M + ((size_t)midx * nchan + n) * a.NHP;
-    double2 tw = w0;
-#pragma unroll 2
-    for (int i = 0; i < NPI; ++i) {
-      const int k = lane + 64 * i;
-      if (i > 0) { tw = cmul(tw, wstep); e = cmul(e, estep); }
-      if (k <= N / 2) {
-        const double2 mk = Mr[k], mn = Mr[N - k];
-        double2 xk, xn;
-        rfft_pair<LOGN>(buf, k, tw, xk, xn);
-        const double2 wk = cmul(cmulc(xk, mk), e);
-        const double2 wn = cmul(cmulc(xn, mn), cmul(EN, cconj(e)));
-        if (k < N / 2) buf[N - k] = wn;  // k = 0: W_N goes to the spare slot N
-        buf[k] = wk;
-      }
+    for (int u = 0; u < kMomU; ++u) {
+      const int k = 4 * u + kk;
+      xb[u] = (ok && k <= N) ? Xr[k] : cmk(0.0, 0.0);
     }
-    fft_sync<true>();
-    double* Tn = reinterpret_cast<double*>(a.T + (((size_t)c * 2 + slot) * nchan + n) * kMT);
-    int cnt = kMT;
-    // sweep 0: moments 0..15 (the usual need) with A_2 and A_14
-    double A2, At;
-    {
-      double acc[32];
+    for (int b = 0; b < nblk; ++b) {
+      double2 xn[kMomU];
+      const bool more = b + 1 < nblk;
 #pragma unroll
-      for (int j = 0; j < 32; ++j) acc[j] = 0.0;
-      double a2 = 0.0, at = 0.0;
-#pragma unroll 1
-      for (int i = 0; i < KW; ++i) {
-        const int k = lane + 64 * i;
-        if (k <= N) {
-          const double2 W = buf[k];
-          const double v = (double)k * iKs;
-          const double aw = fabs(W.x) + fabs(W.y);
-          double pw = 1.0;
-#pragma unroll
-          for (int m = 0; m < 16; ++m) {
-            acc[2 * m] = fma(pw, W.x, acc[2 * m]);
-            acc[2 * m + 1] = fma(pw, W.y, acc[2 * m + 1]);
-            if (m == 2) a2 = fma(pw, aw, a2);
-            if (m == 14) at = fma(pw, aw, at);
-            if (m < 15) pw *= v;
-          }
-        }
+      for (int u = 0; u < kMomU; ++u) {
+        const int k = 4 * ((b + 1) * kMomU + u) + kk;
+        xn[u] = (more && ok && k <= N) ? Xr[k] : cmk(0.0, 0.0);
       }
-      // 32 -> 16 -> ... -> 1 value per lane pair: lane L holds value L >> 1
-      double r16[16], r8[8], r4[4], r2[2], r1[1];
-      rs_swap<16, 32>(acc, r16);
-      rs_swap<8, 16>(r16, r8);
-      rs_step<4>(r8, r4, 8, (lane & 8) != 0);
-      rs_step<2>(r4, r2, 4, (lane & 4) != 0);
-      rs_step<1>(r2, r1, 2, (lane & 2) != 0);
-      r1[0] += __shfl_xor(r1[0], 1);
-      if ((lane & 1) == 0) Tn[lane >> 1] = r1[0];
-      A2 = wave_sum(a2);
-      At = wave_sum(at);
-    }
-    if (!(At * taylor_tail_factor(14) <= 0x1p-57 * A2)) {
-      // sweeps 1, 2: moments 16..23, 24..31 while the bound is not met
-#pragma unroll 1
-      for (int ch = 2; ch < 4; ++ch) {
-        double acc[16];
+      double2 e = turn_phasor((double)(4 * b * kMomU + kk), phic);
 #pragma unroll
-        for (int j = 0; j < 16; ++j) acc[j] = 0.0;
-        double at = 0.0;
-#pragma unroll 1
-        for (int i = 0; i < KW; ++i) {
-          const int k = lane + 64 * i;
-          if (k <= N) {
-            const double2 W = buf[k];
-            const double v = (double)k * iKs;
-            const double v2 = v * v, v4 = v2 * v2, v8 = v4 * v4, v16 = v8 * v8;
-            double pw = ch == 2 ? v16 : v16 * v8;
-            const double aw = fabs(W.x) + fabs(W.y);
-#pragma unroll
-            for (int m = 0; m < 8; ++m) {
-              acc[2 * m] = fma(pw, W.x, acc[2 * m]);
-              acc[2 * m + 1] = fma(pw, W.y, acc[2 * m + 1]);
-              if (m == 6) at = fma(pw, aw, at);
-              if (m < 7) pw *= v;
-            }
-          }
-        }
-        // 16 -> 8 -> 4 -> 2 -> 1 values per lane, then lane bits 1, 0
-        double r8[8], r4[4], r2[2], r1[1];
-        rs_swap<8, 32>(acc, r8);
-        rs_swap<4, 16>(r8, r4);
-        rs_step<2>(r4, r2, 8, (lane & 8) != 0);
-        rs_step<1>(r2, r1, 4, (lane & 4) != 0);
-        r1[0] += __shfl_xor(r1[0], 2);
-        r1[0] += __shfl_xor(r1[0], 1);
-        if ((lane & 3) == 0) Tn[16 * ch + (lane >> 2)] = r1[0];
-        At = wave_sum(at);
-        if (At * taylor_tail_factor(8 * ch + 6) <= 0x1p-57 * A2 || ch == 3) {
-          cnt = 8 * ch + 8;
-          break;
-        }
+      for (int u = 0; u < kMomU; ++u) {
+        const double v = (double)(4 * (b * kMomU + u) + kk) * iN;
+        const double v2 = v * v, v4 = v2 * v2, v8 = v4 * v4;
+        double pc = (col & 1) ? v : 1.0;
+        pc *= (col & 2) ? v2 : 1.0;
+        pc *= (col & 4) ? v4 : 1.0;
+        pc *= (col & 8) ? v8 : 1.0;
+        const double pc16 = pc * (v8 * v8);
+        const double2 W = cmul(xb[u], e);
+        const double bv = part ? W.y : W.x;
+        d0 = __builtin_amdgcn_mfma_f64_16x16x4f64(pc, bv, d0, 0, 0, 0);
+        d1 = __builtin_amdgcn_mfma_f64_16x16x4f64(pc16, bv, d1, 0, 0, 0);
+        e = cmul(e, s4);
       }
-    } else {
-      cnt = 16;
+#pragma unroll
+      for (int u = 0; u < kMomU; ++u) xb[u] = xn[u];
     }
-    if (lane == 0) a.Tcnt[((size_t)c * 2 + slot) * nchan + n] = cnt;
-    fft_sync<true>();  // every lane is done with buf before the next row lands
-    n = nn;
+    // D[row = moment (l >> 4) + 4 r][col = l & 15]
+    if (ok) {
+      double* Tn = reinterpret_cast<double*>(a.T + (((size_t)c * 2 + slot) * nchan + n) * kMT);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        Tn[2 * (kk + 4 * r) + part] = d0[r];
+        Tn[2 * (16 + kk + 4 * r) + part] = d1[r];
+      }
+      if (kk == 0 && part == 0) a.Tcnt[((size_t)c * 2 + slot) * nchan + n] = kMT;
+    }
   }
-  if (tid == 0) st.mvalid |= 1 << slot;
 }
 
 // ---------------------------------------------------------------------------
-// k_solve_taylor: k_solve<false> (ppfit_fit.hip) with every evaluation a
-// Taylor series about one of the subint's two stored centres.  Same scipy
-// trust-ncg control flow, same nfev / status semantics.
+// k_fit_taylor: one workgroup per phase-family subint, the whole fit:
+//   guess_subint (get_TOAs initial phase, pptoas.py:420-456)
+//   moments_from_X about the start point
+//   scipy trust-ncg (k_solve<false>'s control flow, same nfev / status) with
+//     every evaluation a Taylor series; a proposal outside the radius of
+//     both stored centres gets its own centre (one more pass over X) first
+//   post_subint<false> (nu_zero, outputs at nu_out, with-scales covariance)
 // ---------------------------------------------------------------------------
 struct TaylorShared {
   double x[5], xp[5];
   double out[48];
   double red[kWaves][48];
-  int done, nok, slot, park, tslot;
+  int done, nok, slot, tslot;
 };
 
 __device__ __forceinline__ int pick_centre(const FitArgs& a, const Meta& m, const SolveState& st,
@@ -282,36 +176,56 @@ __device__ __forceinline__ int pick_centre(const FitArgs& a, const Meta& m, cons
   return best;
 }
 
-__global__ __launch_bounds__(kBlock) void k_solve_taylor(FitArgs a) {
+union FitShared {
+  GuessShared gs;
+  TaylorShared ts;
+  PostShared ps;
+};
+
+__global__ __launch_bounds__(kBlock) void k_fit_taylor(FitArgs a) {
   extern __shared__ __align__(16) unsigned char dyn[];
-  __shared__ TaylorShared sh;
+  __shared__ FitShared u;
   __shared__ double refs[3];
   const int c = blockIdx.x, s = a.sub0 + c, tid = threadIdx.x;
   const int lane = tid & 63;
+  if (!fused_taylor(a, s)) return;
+  // diagnostic phase clock (ppf_phase_profile): thread 0 only
+  const bool prof = a.ptime != nullptr;
+  unsigned long long t0 = prof ? wall_clock64() : 0ull;
+  unsigned long long pt[5] = {0, 0, 0, 0, 0};
+  unsigned long long nrc = 0;
+  auto mark = [&](int i) {
+    if (prof && tid == 0) {
+      const unsigned long long t1 = wall_clock64();
+      pt[i] += t1 - t0;
+      t0 = t1;
+    }
+  };
+  unsigned char* dmeta = dyn;
+  unsigned char* dguess = dyn + ((meta_bytes(a.nchan) + 255) & ~(size_t)255);
+  guess_subint(a, c, s, dguess, u.gs);
+  __syncthreads();
+  mark(0);
   SolveState& st = a.st[c];
-  if (!st.taylor || st.fin) return;
-  const Meta m = load_meta(a, c, s, dyn, &sh.nok);
+  TaylorShared& sh = u.ts;
+  const Meta m = load_meta(a, c, s, dmeta, &sh.nok);
   const double P = a.P[s];
   if (tid < 5) sh.x[tid] = st.x[tid];
   if (tid < 3) refs[tid] = st.refs[tid];
-  if (tid == 0) { sh.done = (m.nok == 0); sh.slot = st.slot; sh.park = 0; sh.tslot = st.xslot; }
+  if (tid == 0) { sh.done = (m.nok == 0); sh.slot = 0; sh.tslot = 0; }
   __syncthreads();
+  if (!sh.done) {
+    moments_from_X(a, m, c, s, 0, st.xc[0], refs, P);
+    __syncthreads();
+    if (tid == 0) st.mvalid = 1;
+    __syncthreads();
+  }
+  mark(1);
   double* acc0 = a.acc + (size_t)c * 2 * a.nchan * NACC;
   // wave-0 solver state (lane i < 5 owns component i; scalars are uniform)
   double f = 0.0, g = 0.0, xl = 0.0, Hrow[5] = {0, 0, 0, 0, 0};
   double tr = 1.0, predv = 0.0, pl = 0.0;
   int hits = 0, k = 0, status = (m.nok == 0) ? -1 : 0, nfev = 0;
-  int phase = st.phase;
-  if (tid < 64 && phase == 1) {
-    f = st.fun;
-    g = lane < 5 ? st.g[lane] : 0.0;
-    xl = lane < 5 ? sh.x[lane] : 0.0;
-    if (lane < 5)
-      for (int j = 0; j < 5; ++j) Hrow[j] = st.H[lane * 5 + j];
-    tr = st.tr;
-    k = st.kit;
-    nfev = st.nfev;
-  }
   auto load_fgh = [&](double& ff, double& gg, double (&HH)[5]) {
     ff = sh.out[0];
     gg = lane < 5 ? sh.out[1 + lane] : 0.0;
@@ -322,43 +236,36 @@ __global__ __launch_bounds__(kBlock) void k_solve_taylor(FitArgs a) {
       if (lane == pair_j(p)) HH[pair_i(p)] = v;
     }
   };
-  // Park: save the wave-0 state, queue a recentre at p, leave.
-  auto park = [&](const double* p) {
-    if (tid < 64) {
-      if (lane < 5) {
-        st.g[lane] = g;
-        for (int j = 0; j < 5; ++j) st.H[lane * 5 + j] = Hrow[j];
-      }
-      if (lane == 0) {
-        st.fun = f;
-        st.tr = tr;
-        st.kit = k;
-        st.nfev = nfev;
-        st.phase = phase;
-        st.slot = sh.slot;
-        st.xslot = sh.tslot;
-        const int wsl = sh.tslot ^ 1;
-        st.wslot = wsl;
-        st.mvalid &= ~(1 << wsl);
-        for (int i = 0; i < 5; ++i) { st.xc[wsl][i] = p[i]; st.x[i] = sh.x[i]; }
-        const int q = atomicAdd(a.rq_count, 1);
-        a.rq_list[q] = c;
-      }
+  // a centre that covers p: a stored one, else p itself (one more X pass)
+  auto centre_for = [&](const double* p, TaylorSrc& ts) -> int {
+    int q = pick_centre(a, m, st, c, p, refs, P, sh.red[0], ts);
+    if (q >= 0) return q;
+    const int wsl = sh.tslot ^ 1;
+    ++nrc;
+    if (tid == 0) {
+      st.mvalid &= ~(1 << wsl);
+      for (int i = 0; i < 5; ++i) st.xc[wsl][i] = p[i];
     }
+    __syncthreads();
+    moments_from_X(a, m, c, s, wsl, st.xc[wsl], refs, P);
+    __syncthreads();
+    if (tid == 0) st.mvalid |= 1 << wsl;
+    __syncthreads();
+    q = pick_centre(a, m, st, c, p, refs, P, sh.red[0], ts);
+    return q;  // p is that centre: |y| = 0
   };
-  if (!sh.done && phase == 0) {
+  if (!sh.done) {
     TaylorSrc ts{};
-    const int q = pick_centre(a, m, st, c, sh.x, refs, P, sh.red[0], ts);
-    if (q < 0) { park(sh.x); return; }
-    sweep<0, false>(a, m, c, s, sh.x, refs, P, acc0 + (size_t)sh.slot * a.nchan * NACC, sh.out,
-                    sh.red, ts);
+    const int q = centre_for(sh.x, ts);
+    mark(2);
+    sweep<0, false>(a, m, c, s, sh.x, refs, P, acc0, sh.out, sh.red, ts);
+    mark(3);
     if (tid < 64) {
       load_fgh(f, g, Hrow);
       xl = lane < 5 ? sh.x[lane] : 0.0;
       nfev = 1;
     }
     if (tid == 0) sh.tslot = q;
-    phase = 1;
   }
   while (!sh.done) {
     if (tid < 64) {
@@ -373,16 +280,14 @@ __global__ __launch_bounds__(kBlock) void k_solve_taylor(FitArgs a) {
       }
     }
     __syncthreads();
+    mark(4);
     if (sh.done) break;
     TaylorSrc ts{};
-    const int q = pick_centre(a, m, st, c, sh.xp, refs, P, sh.red[0], ts);
-    if (q < 0) {
-      // the proposal is recomputed bit-identically from the saved state on resume
-      park(sh.xp);
-      return;
-    }
+    const int q = centre_for(sh.xp, ts);
+    mark(2);
     double* sl = acc0 + (size_t)(sh.slot ^ 1) * a.nchan * NACC;
     sweep<0, false>(a, m, c, s, sh.xp, refs, P, sl, sh.out, sh.red, ts);
+    mark(3);
     if (tid < 64) {
       double fp, gp, Hp[5] = {0, 0, 0, 0, 0};
       load_fgh(fp, gp, Hp);
@@ -423,6 +328,12 @@ __global__ __launch_bounds__(kBlock) void k_solve_taylor(FitArgs a) {
     st.xslot = sh.tslot;
     st.fin = 1;
     st.scat_post = false;
+    if (prof) {
+#pragma unroll
+      for (int i = 0; i < 5; ++i) atomicAdd(&a.ptime[i], pt[i]);
+      atomicAdd(&a.ptime[8], nrc);
+      atomicAdd(&a.ptime[9], 1ull);
+    }
   }
 }
 
@@ -446,17 +357,22 @@ __global__ void k_selftest(int* fails) {
   chk(6, wave_max(x * (l == 37 ? 2.0 : 1.0)) == 74.0);
   chk(7, lane0(x + 3.0) == 3.0 && lane_at<4>(x) == 4.0);
   chk(8, dpp_mov<0xB1>(x) == (double)(l ^ 1) && dpp_mov<0x4E>(x) == (double)(l ^ 2));
+  // v_mfma_f64_16x16x4: A[i][k] = i + 1 + 16 k, B[k][j] = 2 j + 3 k + 1
+  {
+    const int i = l & 15, kq = l >> 4;
+    f64x4 d = {0.0, 0.0, 0.0, 0.0};
+    d = __builtin_amdgcn_mfma_f64_16x16x4f64((double)(i + 1 + 16 * kq),
+                                             (double)(2 * i + 3 * kq + 1), d, 0, 0, 0);
+    bool ok = true;
+    for (int r = 0; r < 4; ++r) {
+      const int row = kq + 4 * r;
+      double ref = 0.0;
+      for (int q = 0; q < 4; ++q) ref += (double)(row + 1 + 16 * q) * (double)(2 * i + 3 * q + 1);
+      ok = ok && d[r] == ref;
+    }
+    chk(9, ok);
+  }
 }
 
-#define PPF_INST_TAYLOR(L) template __global__ void k_moments<L>(FitArgs);
-PPF_INST_TAYLOR(5)
-PPF_INST_TAYLOR(6)
-PPF_INST_TAYLOR(7)
-PPF_INST_TAYLOR(8)
-PPF_INST_TAYLOR(9)
-PPF_INST_TAYLOR(10)
-PPF_INST_TAYLOR(11)
-PPF_INST_TAYLOR(12)
-#undef PPF_INST_TAYLOR
 
 }  // namespace ppf

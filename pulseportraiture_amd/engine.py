@@ -115,6 +115,13 @@ class Engine:
                                                ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value
 
+    def phase_profile(self, enable):
+        """k_fit_taylor phase clocks accumulated since the last call (ticks of
+        wall_clock64, 100 MHz) as a list of PPF_PHASE_N ints; sets enable."""
+        out = (ctypes.c_uint64 * _lib.PPF_PHASE_N)()
+        self._chk(self.lib.ppf_phase_profile(self.ctx, int(bool(enable)), out))
+        return list(out)
+
     def selftest(self):
         """Device check of the cross-lane primitives (DPP, permlane swaps);
         returns the per-test failing-lane counts (all 0 = pass)."""

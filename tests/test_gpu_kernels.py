@@ -27,7 +27,7 @@ NBINS = [64, 128, 256, 512, 1024, 2048, 4096, 8192]
 
 def test_cross_lane_selftest(eng):
     """DPP / permlane16,32 swap / readlane semantics the reductions rely on."""
-    assert eng.selftest() == [0] * 9
+    assert eng.selftest() == [0] * 10
 
 
 @pytest.mark.parametrize("nbin", NBINS)

@@ -44,8 +44,22 @@ def _pair(eng, w, data, flags, init, mask=None, guess=True, **kw):
     return t, e
 
 
+def _statuses_agree(t, e):
+    """Identical status, except for scipy's exact-zero-gradient stop: when the
+    gradient at the accepted point rounds to exactly 0.0, Steihaug CG returns
+    a NaN step (0/0 in get_boundaries_intersections), no proposal is ever
+    accepted and trust-ncg ends at maxiter (status 1, nfev 1001) -- as the
+    reference does on the same rounding.  Whether the last Newton step lands
+    on a point whose float gradient is exactly 0 depends on summation order
+    (observed ~1 in 10^3 converged subints), so the two device paths may
+    differ there while their parameters agree to rounding."""
+    for i in np.where(t["status"] != e["status"])[0]:
+        pair = {int(t["status"][i]), int(e["status"][i])}
+        assert pair == {1, 2} and max(t["nfev"][i], e["nfev"][i]) == 1001, (i, pair)
+
+
 def _assert_close(t, e, flags, tol=1e-4):
-    np.testing.assert_array_equal(t["status"], e["status"])
+    _statuses_agree(t, e)
     assert np.mean(t["nfev"] == e["nfev"]) >= 0.5, (t["nfev"], e["nfev"])
     for i in range(5):
         if flags[i]:
