@@ -728,7 +728,7 @@ __device__ void guess_subint(const FitArgs& a, int c, int s, unsigned char* dyn,
   // err = get_noise(rot_prof) * sqrt(nbin/2), pplib.py:2076-2080
   const double noise = sqrt(pno / (double)a.nbin / (double)(a.NH - a.kc));
   const double err2 = noise * noise * (0.5 * (double)a.nbin);
-  guess_search(rm, a.NH, 1.0 / err2, a.Ns, -0.5, 0.5, gs);
+  guess_search(rm, a.NH, 1.0 / err2, a.Ns, -0.5, 0.5, gs, a.ptime ? a.ptime + 10 : nullptr);
   if (tid == 0) {
     double nug = a.guess_nu ? a.guess_nu[s] : NAN;
     if (isnan(nug)) nug = fmean;

@@ -121,24 +121,9 @@ struct GuessShared {
   int besti[kWaves];
   double x0, x, fx;
   double out[8];
+  double bf[kBlock];       // brute force: partial sums per (half, grid point)
+  double ev[2][kWaves];    // Nelder-Mead: per-wave partials, double-buffered
 };
-
-// One wave evaluates sum_k Re(rm_k e^{2 pi i k phi}); every lane gets it.
-__device__ __forceinline__ double wave_eval_phase(const double2* rm, int NH, double phi) {
-  const int lane = threadIdx.x & 63;
-  const double2 step = turn_phasor(64.0, phi);
-  double2 e = cmk(1.0, 0.0);
-  double acc = 0.0;
-  int j = 0;
-  for (int k = lane; k < NH; k += 64, ++j) {
-    if ((j & 15) == 0) e = turn_phasor((double)k, phi);
-    else e = cmul(e, step);
-    const double2 r = rm[k];
-    acc = fma(r.x, e.x, acc);
-    acc = fma(-r.y, e.y, acc);
-  }
-  return wave_sum(acc);
-}
 
 // np.argmin order: the first NaN wins, else the first smallest value.
 __device__ __forceinline__ bool argmin_better(double v, int i, double bv, int bi) {
@@ -149,39 +134,113 @@ __device__ __forceinline__ bool argmin_better(double v, int i, double bv, int bi
   return v < bv || (v == bv && i < bi);
 }
 
-__device__ inline void guess_search(const double2* rm, int NH, double ie2, int Ns, double lo,
-                                    double hi, GuessShared& gs) {
+// Sum over k in [k0, k1) of Re(rm_k e^{2 pi i k phi}) by one thread: the
+// phasor advances by e^{2 pi i phi} per harmonic and is re-seeded exactly
+// (turn_phasor) every 64 harmonics.
+__device__ __forceinline__ double row_eval_phase(const double2* rm, int k0, int k1, double phi) {
+  const double2 z = turn_phasor(1.0, phi);
+  double acc = 0.0;
+  for (int kb = k0; kb < k1; kb += 64) {
+    double2 e = turn_phasor((double)kb, phi);
+    const int ke = min(kb + 64, k1);
+#pragma unroll 4
+    for (int k = kb; k < ke; ++k) {
+      const double2 r = rm[k];  // same address in every lane: LDS broadcast
+      acc = fma(r.x, e.x, acc);
+      acc = fma(-r.y, e.y, acc);
+      e = cmul(e, z);
+    }
+  }
+  return acc;
+}
+
+// All threads of the block evaluate sum_k Re(rm_k e^{2 pi i k phi}) together
+// (thread t takes k = t, t + kBlock, ...); every thread returns the same
+// value (fixed cross-wave order).  par: the LDS slot pair to use, alternated
+// by the caller so that one barrier per evaluation suffices.
+__device__ __forceinline__ double block_eval_phase(const double2* rm, int NH, double phi,
+                                                   double* slot) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const double2 st = turn_phasor((double)kBlock, phi);
+  double2 e = turn_phasor((double)tid, phi);
+  double acc = 0.0;
+  for (int k = tid; k < NH; k += kBlock) {
+    const double2 r = rm[k];
+    acc = fma(r.x, e.x, acc);
+    acc = fma(-r.y, e.y, acc);
+    e = cmul(e, st);
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) slot[w] = acc;
+  __syncthreads();
+  double t = slot[0];
+#pragma unroll
+  for (int q = 1; q < kWaves; ++q) t += slot[q];
+  return t;
+}
+
+__device__ inline void guess_search(const double2* rm, int NH, double ie2, int Ns, double lo,
+                                    double hi, GuessShared& gs,
+                                    unsigned long long* clk = nullptr) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // diagnostic clocks (ppf_phase_profile): [0] brute force, [1] Nelder-Mead, [2] NM calls
+  const unsigned long long c0 = clk ? wall_clock64() : 0ull;
   // ---- brute force over the inclusive grid (np.mgrid[lo:hi:Ns*1j]) ----
   // grid and simplex arithmetic use explicit _rn ops: hipcc would otherwise
   // contract them into FMAs and move the points off numpy's values.
+  // Threads own grid points (kBlock / 2 per chunk) and walk half of the
+  // harmonics each; the halves meet in LDS.
+  constexpr int GP = kBlock / 2;
   const double step = (hi - lo) / (double)(Ns - 1);
+  const int half = tid / GP, gl = tid % GP;
+  const int kmid = (NH + 1) / 2;
   double bv = NAN;
   int bi = 0x7fffffff;
-  for (int g = w; g < Ns; g += kWaves) {  // ascending per wave
-    const double ph = (g == Ns - 1) ? hi : __dadd_rn(__dmul_rn((double)g, step), lo);
-    const double f = -wave_eval_phase(rm, NH, ph) * ie2;
-    if (argmin_better(f, g, bv, bi)) { bv = f; bi = g; }
+  for (int g0 = 0; g0 < Ns; g0 += GP) {
+    const int g = g0 + gl;
+    double part = 0.0;
+    if (g < Ns) {
+      const double ph = (g == Ns - 1) ? hi : __dadd_rn(__dmul_rn((double)g, step), lo);
+      part = half ? row_eval_phase(rm, kmid, NH, ph) : row_eval_phase(rm, 0, kmid, ph);
+    }
+    gs.bf[tid] = part;
+    __syncthreads();
+    if (tid < GP && g < Ns) {
+      const double f = -(gs.bf[tid] + gs.bf[GP + tid]) * ie2;
+      if (argmin_better(f, g, bv, bi)) { bv = f; bi = g; }
+    }
+    __syncthreads();
   }
-  if (lane == 0) { gs.bestv[w] = bv; gs.besti[w] = bi; }
+  // argmin over the owning threads (ascending g within a thread)
+  if (tid < GP) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const double ov = __shfl_xor(bv, o);
+      const int oi = __shfl_xor(bi, o);
+      if (argmin_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+    }
+    if (lane == 0) { gs.bestv[w] = bv; gs.besti[w] = bi; }
+  }
   __syncthreads();
   if (tid == 0) {
     double v = gs.bestv[0];
     int i = gs.besti[0];
-    for (int q = 1; q < kWaves; ++q)
+    for (int q = 1; q < GP / 64; ++q)
       if (argmin_better(gs.bestv[q], gs.besti[q], v, i)) { v = gs.bestv[q]; i = gs.besti[q]; }
     gs.x0 = (i == Ns - 1) ? hi : __dadd_rn(__dmul_rn((double)i, step), lo);
   }
   __syncthreads();
-  // ---- Nelder-Mead polish, wave 0 (uniform scalar control flow) ----
-  if (w == 0) {
+  const unsigned long long c1 = clk ? wall_clock64() : 0ull;
+  // ---- Nelder-Mead polish: every thread runs the (uniform, scalar) simplex
+  // logic; each evaluation is one block-wide sum ----
+  {
     const int maxfun = 200, maxiter = 200;
     int fcalls = 0;
     bool stop = false;
     auto F = [&](double xv) -> double {
       if (fcalls >= maxfun) { stop = true; return 0.0; }
       ++fcalls;
-      return -wave_eval_phase(rm, NH, xv) * ie2;
+      return -block_eval_phase(rm, NH, xv, gs.ev[fcalls & 1]) * ie2;
     };
     double s0 = gs.x0;
     double s1 = (s0 != 0.0) ? (1.0 + 0.05) * s0 : 0.00025;
@@ -222,7 +281,15 @@ __device__ inline void guess_search(const double2* rm, int NH, double ie2, int N
       if (f1 < f0) { double t = s0; s0 = s1; s1 = t; t = f0; f0 = f1; f1 = t; }
     }
     if (f1 < f0) { double t = s0; s0 = s1; s1 = t; t = f0; f0 = f1; f1 = t; }
-    if (lane == 0) { gs.x = s0; gs.fx = fmin(f0, f1); }
+    if (tid == 0) {
+      gs.x = s0;
+      gs.fx = fmin(f0, f1);
+      if (clk) {
+        atomicAdd(&clk[0], c1 - c0);
+        atomicAdd(&clk[1], wall_clock64() - c1);
+        atomicAdd(&clk[2], (unsigned long long)fcalls);
+      }
+    }
   }
   __syncthreads();
 }

@@ -64,4 +64,6 @@ nwg = max(pt[9], 1)
 print("phase clocks per workgroup (us):",
       {n: round(pt[i] / nwg / 100.0, 2) for i, n in
        enumerate(["guess", "meta+moments0", "centre", "sweep", "trstep"])},
-      "recentres/subint", pt[8] / nwg, "workgroups", pt[9])
+      "recentres/subint", pt[8] / nwg, "workgroups", pt[9],
+      "guess brute/NM us", round(pt[10] / nwg / 100.0, 2), round(pt[11] / nwg / 100.0, 2),
+      "NM calls", pt[12] / nwg)
