@@ -145,7 +145,7 @@ def main():
 
     ktimes = {}
     if not args.no_timing:
-        for name in ["data_xspec", "guess", "fit_taylor", "solve", "post", "model_fft"]:
+        for name in ["data_xspec", "guess", "moments", "fit_taylor", "solve", "post", "model_fft"]:
             ms, n = eng.kernel_time(name)
             ktimes[name] = (ms, n)
         eng.set_timing(False)

@@ -65,7 +65,8 @@ extern "C" {
 #define PPF_K_GUESS 9
 #define PPF_K_POST 10
 #define PPF_K_FIT_TAYLOR 11
-#define PPF_NUM_KERNELS 12
+#define PPF_K_MOMENTS 12
+#define PPF_NUM_KERNELS 13
 
 typedef struct ppf_ctx ppf_ctx;
 

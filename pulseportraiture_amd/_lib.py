@@ -14,7 +14,7 @@ PPF_OK = 0
 PPF_METHOD_TRUST_NCG = 0
 KERNEL_IDS = {"model_fft": 0, "data_xspec": 1, "solve": 2, "phase_shift": 3,
               "rotate": 4, "rot_accum": 5, "synth": 6, "irfft": 7, "noise": 8,
-              "guess": 9, "post": 10, "fit_taylor": 11}
+              "guess": 9, "post": 10, "fit_taylor": 11, "moments": 12}
 PPF_SOLVE_EXACT = 1
 PPF_SELFTEST_N = 10
 PPF_PHASE_N = 16

@@ -439,9 +439,13 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
         }))
       return r;
     if (taylor) {
+      if (int r = timed(ctx, PPF_K_MOMENTS, [&] {
+            hipLaunchKernelGGL(k_moments, dim3(nc, (nchan + 8 * kWaves - 1) / (8 * kWaves)),
+                               dim3(kBlock), 0, ctx->stream, fa);
+          }))
+        return r;
       if (int r = timed(ctx, PPF_K_FIT_TAYLOR, [&] {
-            hipLaunchKernelGGL(k_fit_taylor, dim3(nc), dim3(kBlock), lds_meta + lds_guess,
-                               ctx->stream, fa);
+            hipLaunchKernelGGL(k_fit_taylor, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
           }))
         return r;
     }

@@ -748,14 +748,6 @@ __global__ __launch_bounds__(kBlock) void k_guess(FitArgs a) {
   extern __shared__ __align__(16) unsigned char dyn[];
   __shared__ GuessShared gs;
   const int c = blockIdx.x, s = a.sub0 + c;
-  if (fused_taylor(a, s)) {  // k_fit_taylor owns this subint: keep the
-    if (threadIdx.x == 0) {  // exact-path kernels launched around it off it
-      a.st[c].scat = 0;
-      a.st[c].scat_post = 0;
-      a.st[c].taylor = 1;
-    }
-    return;
-  }
   guess_subint(a, c, s, dyn, gs);
 }
 

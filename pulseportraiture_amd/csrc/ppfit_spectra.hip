@@ -173,16 +173,29 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
     if (lane == 0) s_act[w] = act;
     if (act && !have) row.load(drow0 + (size_t)n * 2 * N, lane);
     have = false;
+    // template harmonics k and N - k of this row, in flight during the FFT
+    // (M is shared by every subint: L2-resident)
+    const double2* Mr = a.M + ((size_t)midx * nchan + (act ? n : 0)) * a.NHP;
+    // rolling prefetch two pair iterations deep: (m0k, m0n) for iteration i,
+    // (m1k, m1n) for i + 1; the first two are issued before the FFT
+    auto mload = [&](int i, double2& mk, double2& mn) {
+      const int k = lane + 64 * i;
+      if (i < NPI && k <= N / 2) { mk = Mr[k]; mn = Mr[N - k]; }
+    };
+    double2 m0k = cmk(0.0, 0.0), m0n = m0k, m1k = m0k, m1n = m0k;
     if (act) {
       row.store(buf, drow0 + (size_t)n * 2 * N, lane);
+      mload(0, m0k, m0n);
+      mload(1, m1k, m1n);
+      fft_sync<true>();
+      wave_fft<LOGN>(buf, twl, lane);
     }
+    // next row of this wave streams in during the spectrum pass
     if (active(n + WPB)) {
       row.load(drow0 + (size_t)(n + WPB) * 2 * N, lane);
       have = true;
     }
     if (act) {
-      fft_sync<true>();
-      wave_fft<LOGN>(buf, twl, lane);
       const double2 cm = cmeta[n];
       const double wgt = cm.y;
       double2 e = cmk(1.0, 0.0), estep = e, EN = e;
@@ -191,7 +204,6 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
         estep = turn_phasor(64.0, cm.x);
         EN = turn_phasor((double)N, cm.x);
       }
-      const double2* Mr = a.M + ((size_t)midx * nchan + n) * a.NHP;
       double2* Xr = wx ? a.X + ((size_t)c * nchan + n) * a.NHP : nullptr;
       double pn = 0.0, pd = 0.0;
       double2 tw = w0;
@@ -199,6 +211,10 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
       for (int i = 0; i < NPI; ++i) {
         const int k = lane + 64 * i;
         if (i > 0) { tw = cmul(tw, wstep); e = cmul(e, estep); }
+        const double2 mk = m0k, mn = m0n;
+        m0k = m1k;
+        m0n = m1n;
+        mload(i + 2, m1k, m1n);
         if (k <= N / 2) {
           double2 xk, xn;
           rfft_pair<LOGN>(buf, k, tw, xk, xn);
@@ -210,8 +226,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
           if (k >= 1) pd += p2k;
           if (two) pd += p2n;
           if (wx) {
-            Xr[k] = (k == 0) ? cmk(0.0, 0.0) : cmulc(xk, Mr[k]);
-            if (two) Xr[kn] = cmulc(xn, Mr[kn]);
+            Xr[k] = (k == 0) ? cmk(0.0, 0.0) : cmulc(xk, mk);
+            if (two) Xr[kn] = cmulc(xn, mn);
           }
           if (a.guess) {
             // e^{2 pi i (N-k) phi} = e^{2 pi i N phi} conj(e^{2 pi i k phi});
@@ -224,7 +240,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
         }
       }
       if (wx)
-        for (int k = NH + lane; k < a.NHP; k += 64) Xr[k] = cmk(0.0, 0.0);
+      for (int k = NH + lane; k < a.NHP; k += 64) Xr[k] = cmk(0.0, 0.0);
       pn = wave_sum(pn);
       pd = wave_sum(pd);
       if (lane == 0) {

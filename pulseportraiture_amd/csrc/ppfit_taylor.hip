@@ -79,69 +79,105 @@ __device__ __forceinline__ void rs_swap(const double* v, double* out) {
 // kept (cnt = kMT): the truncation bound then holds for any spectrum.
 // ---------------------------------------------------------------------------
 typedef double f64x4 __attribute__((ext_vector_type(4)));
-constexpr int kMomU = 8;
 
-__device__ void moments_from_X(const FitArgs& a, const Meta& m, int c, int s, int slot,
-                               const double* xc, const double* refs, double P) {
+// One 8-channel tile by one wave: lane l handles channel n (of column
+// (l & 15) >> 1; ok = fitted) with centre phase phic; U = steps in flight.
+template <int U>
+__device__ __forceinline__ void moment_tile(const FitArgs& a, int c, int slot, int n, bool ok,
+                                            double phic) {
   static_assert(kMT == 32, "two 16-row MFMA tiles");
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int nchan = a.nchan;
+  const int lane = threadIdx.x & 63;
   const int N = a.nbin / 2;
   const double iN = 1.0 / (double)N;
-  const int nblk = ((N + 1 + 3) / 4 + kMomU - 1) / kMomU;  // blocks of kMomU 4-harmonic steps
-  const int col = lane & 15, chl = col >> 1, part = col & 1, kk = lane >> 4;
+  const int nblk = ((N + 1 + 3) / 4 + U - 1) / U;  // blocks of U 4-harmonic steps
+  const int col = lane & 15, part = col & 1, kk = lane >> 4;
+  const double2* __restrict__ Xr = a.X + ((size_t)c * a.nchan + (ok ? n : 0)) * a.NHP;
+  const double2 s4 = turn_phasor(4.0, phic);
+  // two accumulator pairs (even / odd steps): independent MFMA chains
+  f64x4 d0 = {0.0, 0.0, 0.0, 0.0}, d1 = d0, d2 = d0, d3 = d0;
+  double2 xb[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int k = 4 * u + kk;
+    xb[u] = (ok && k <= N) ? Xr[k] : cmk(0.0, 0.0);
+  }
+  for (int b = 0; b < nblk; ++b) {
+    double2 xn[U];
+    const bool more = b + 1 < nblk;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = 4 * ((b + 1) * U + u) + kk;
+      xn[u] = (more && ok && k <= N) ? Xr[k] : cmk(0.0, 0.0);
+    }
+    double2 e = turn_phasor((double)(4 * b * U + kk), phic);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const double v = (double)(4 * (b * U + u) + kk) * iN;
+      const double v2 = v * v, v4 = v2 * v2, v8 = v4 * v4;
+      double pc = (col & 1) ? v : 1.0;
+      pc *= (col & 2) ? v2 : 1.0;
+      pc *= (col & 4) ? v4 : 1.0;
+      pc *= (col & 8) ? v8 : 1.0;
+      const double pc16 = pc * (v8 * v8);
+      const double2 W = cmul(xb[u], e);
+      const double bv = part ? W.y : W.x;
+      if (u & 1) {
+        d2 = __builtin_amdgcn_mfma_f64_16x16x4f64(pc, bv, d2, 0, 0, 0);
+        d3 = __builtin_amdgcn_mfma_f64_16x16x4f64(pc16, bv, d3, 0, 0, 0);
+      } else {
+        d0 = __builtin_amdgcn_mfma_f64_16x16x4f64(pc, bv, d0, 0, 0, 0);
+        d1 = __builtin_amdgcn_mfma_f64_16x16x4f64(pc16, bv, d1, 0, 0, 0);
+      }
+      e = cmul(e, s4);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) xb[u] = xn[u];
+  }
+  d0 += d2;
+  d1 += d3;
+  // D[row = moment (l >> 4) + 4 r][col = l & 15]
+  if (ok) {
+    double* Tn = reinterpret_cast<double*>(a.T + (((size_t)c * 2 + slot) * a.nchan + n) * kMT);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      Tn[2 * (kk + 4 * r) + part] = d0[r];
+      Tn[2 * (16 + kk + 4 * r) + part] = d1[r];
+    }
+    if (kk == 0 && part == 0) a.Tcnt[((size_t)c * 2 + slot) * a.nchan + n] = kMT;
+  }
+}
+
+// All fitted channels of subint c, all threads of the block (recentring).
+__device__ void moments_from_X(const FitArgs& a, const Meta& m, int c, int s, int slot,
+                               const double* xc, const double* refs, double P) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int chl = (lane & 15) >> 1;
   for (int t = w; t * 8 < m.nok; t += kWaves) {
     const int j = t * 8 + chl;
     const bool ok = j < m.nok;
-    const int n = ok ? m.chan[j] : 0;
-    const double2* __restrict__ Xr = a.X + ((size_t)c * nchan + n) * a.NHP;
-    const double phic = ok ? phase_frac(xc, m.fr[j], refs, P) : 0.0;
-    const double2 s4 = turn_phasor(4.0, phic);
-    f64x4 d0 = {0.0, 0.0, 0.0, 0.0}, d1 = {0.0, 0.0, 0.0, 0.0};
-    double2 xb[kMomU];
-#pragma unroll
-    for (int u = 0; u < kMomU; ++u) {
-      const int k = 4 * u + kk;
-      xb[u] = (ok && k <= N) ? Xr[k] : cmk(0.0, 0.0);
-    }
-    for (int b = 0; b < nblk; ++b) {
-      double2 xn[kMomU];
-      const bool more = b + 1 < nblk;
-#pragma unroll
-      for (int u = 0; u < kMomU; ++u) {
-        const int k = 4 * ((b + 1) * kMomU + u) + kk;
-        xn[u] = (more && ok && k <= N) ? Xr[k] : cmk(0.0, 0.0);
-      }
-      double2 e = turn_phasor((double)(4 * b * kMomU + kk), phic);
-#pragma unroll
-      for (int u = 0; u < kMomU; ++u) {
-        const double v = (double)(4 * (b * kMomU + u) + kk) * iN;
-        const double v2 = v * v, v4 = v2 * v2, v8 = v4 * v4;
-        double pc = (col & 1) ? v : 1.0;
-        pc *= (col & 2) ? v2 : 1.0;
-        pc *= (col & 4) ? v4 : 1.0;
-        pc *= (col & 8) ? v8 : 1.0;
-        const double pc16 = pc * (v8 * v8);
-        const double2 W = cmul(xb[u], e);
-        const double bv = part ? W.y : W.x;
-        d0 = __builtin_amdgcn_mfma_f64_16x16x4f64(pc, bv, d0, 0, 0, 0);
-        d1 = __builtin_amdgcn_mfma_f64_16x16x4f64(pc16, bv, d1, 0, 0, 0);
-        e = cmul(e, s4);
-      }
-#pragma unroll
-      for (int u = 0; u < kMomU; ++u) xb[u] = xn[u];
-    }
-    // D[row = moment (l >> 4) + 4 r][col = l & 15]
-    if (ok) {
-      double* Tn = reinterpret_cast<double*>(a.T + (((size_t)c * 2 + slot) * nchan + n) * kMT);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        Tn[2 * (kk + 4 * r) + part] = d0[r];
-        Tn[2 * (16 + kk + 4 * r) + part] = d1[r];
-      }
-      if (kk == 0 && part == 0) a.Tcnt[((size_t)c * 2 + slot) * nchan + n] = kMT;
-    }
+    moment_tile<8>(a, c, slot, ok ? m.chan[j] : 0, ok,
+                   ok ? phase_frac(xc, m.fr[j], refs, P) : 0.0);
   }
+}
+
+// ---------------------------------------------------------------------------
+// k_moments: the first moment pass of every phase-family subint, about its
+// start point st.xc[0] (k_guess), into T slot 0 -- a pure stream over X at
+// full occupancy.  Block (c, y): wave w takes channels 8 (4 y + w) .. + 7
+// (masked channels idle in their lane).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_moments(FitArgs a) {
+  const int c = blockIdx.x, s = a.sub0 + c;
+  if (!fused_taylor(a, s)) return;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int n0 = 8 * (kWaves * (int)blockIdx.y + w);
+  if (n0 >= a.nchan) return;  // whole wave
+  const SolveState& st = a.st[c];
+  const int n = n0 + ((lane & 15) >> 1);
+  const bool ok = n < a.nchan && (!a.mask || a.mask[(size_t)s * a.nchan + n]);
+  const double phic = ok ? phase_frac(st.xc[0], a.freqs[(size_t)s * a.nchan + n], st.refs, a.P[s])
+                         : 0.0;
+  moment_tile<16>(a, c, 0, n, ok, phic);
 }
 
 // ---------------------------------------------------------------------------
@@ -202,24 +238,19 @@ __global__ __launch_bounds__(kBlock) void k_fit_taylor(FitArgs a) {
     }
   };
   unsigned char* dmeta = dyn;
-  unsigned char* dguess = dyn + ((meta_bytes(a.nchan) + 255) & ~(size_t)255);
-  guess_subint(a, c, s, dguess, u.gs);
-  __syncthreads();
-  mark(0);
   SolveState& st = a.st[c];
   TaylorShared& sh = u.ts;
   const Meta m = load_meta(a, c, s, dmeta, &sh.nok);
   const double P = a.P[s];
   if (tid < 5) sh.x[tid] = st.x[tid];
   if (tid < 3) refs[tid] = st.refs[tid];
-  if (tid == 0) { sh.done = (m.nok == 0); sh.slot = 0; sh.tslot = 0; }
-  __syncthreads();
-  if (!sh.done) {
-    moments_from_X(a, m, c, s, 0, st.xc[0], refs, P);
-    __syncthreads();
-    if (tid == 0) st.mvalid = 1;
-    __syncthreads();
+  if (tid == 0) {
+    sh.done = (m.nok == 0);
+    sh.slot = 0;
+    sh.tslot = 0;
+    st.mvalid = 1;  // slot 0: k_moments, about st.xc[0]
   }
+  __syncthreads();
   mark(1);
   double* acc0 = a.acc + (size_t)c * 2 * a.nchan * NACC;
   // wave-0 solver state (lane i < 5 owns component i; scalars are uniform)

@@ -22,7 +22,7 @@ P = torch.full((nsub,), w.P, dtype=torch.float64, device=dev)
 nu = torch.full((nsub, 3), pplib.guess_fit_freq(w.freqs), dtype=torch.float64, device=dev)
 init0 = torch.tensor([[0.0, w.DM0, 0.0, 0.0, 0.0]] * nsub, dtype=torch.float64, device=dev)
 flags = [1, 1, 0, 0, 0]
-names = ["data_xspec", "guess", "fit_taylor", "solve", "post", "model_fft"]
+names = ["data_xspec", "guess", "moments", "fit_taylor", "solve", "post", "model_fft"]
 
 
 def run(init, guess, reps=3):
