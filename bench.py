@@ -44,7 +44,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 # passes over this same bench (tools/profile_r1.sh + tools/pmc_summary.py).
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
 KERNEL_SYMBOL = {"solve": "k_solve<false>", "data_xspec": "k_data_xspec<10>",
-                 "post": "k_post<false>", "guess": "k_guess"}
+                 "post": "k_post<false>", "guess": "k_guess", "moments": "k_moments",
+                 "fit_taylor": "k_fit_taylor"}
 
 
 def pmc_traffic(kernel, nsub, nbin, nchan, config):
@@ -200,13 +201,15 @@ def main():
         from oracle import ppfit_oracle as O
         S = min(args.cpu_sample, nsub)
         dh = data[:S].cpu().numpy()
-        t0 = time.perf_counter()
+        from threadpoolctl import threadpool_limits
         refs = []
-        for i in range(S):
-            errs = O.get_noise_PS(dh[i], chans=True)
-            refs.append(O.fit_subint_pptoas(dh[i], w.model, w.freqs, np.ones(nchan), errs,
-                                            np.ones(nchan), w.P, w.DM0, flags))
-        tcpu = time.perf_counter() - t0
+        with threadpool_limits(limits=1):  # the baseline is one core: pin BLAS/OpenMP pools
+            t0 = time.perf_counter()
+            for i in range(S):
+                errs = O.get_noise_PS(dh[i], chans=True)
+                refs.append(O.fit_subint_pptoas(dh[i], w.model, w.freqs, np.ones(nchan), errs,
+                                                np.ones(nchan), w.P, w.DM0, flags))
+            tcpu = time.perf_counter() - t0
         cpu = {"value": round(S / tcpu, 3), "unit": "TOAs/s", "cores": 1, "kind": "port",
                "sample": "%d of the same synthetic subints (64x2048, get_TOAs guess+fit+"
                          "post-fit incl. noise estimate) in %.1f s, numpy/scipy oracle, "
