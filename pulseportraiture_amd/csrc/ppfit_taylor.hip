@@ -82,56 +82,69 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 // One 8-channel tile by one wave: lane l handles channel n (of column
 // (l & 15) >> 1; ok = fitted) with centre phase phic; U = steps in flight.
+// Steps go in pairs (u, u + 1): lane part p loads X at the harmonic of step
+// u + p, so the 8 lanes of a channel read one whole 128-B line per pair and
+// no element is fetched twice; each lane rotates its own element, keeps the
+// part it needs and trades the other with its partner (DPP quad_perm
+// [1,0,3,2]): partner lanes differ only in p.
 template <int U>
 __device__ __forceinline__ void moment_tile(const FitArgs& a, int c, int slot, int n, bool ok,
                                             double phic) {
   static_assert(kMT == 32, "two 16-row MFMA tiles");
+  static_assert(U % 2 == 0, "steps go in pairs");
+  constexpr int UP = U / 2;
   const int lane = threadIdx.x & 63;
   const int N = a.nbin / 2;
   const double iN = 1.0 / (double)N;
   const int nblk = ((N + 1 + 3) / 4 + U - 1) / U;  // blocks of U 4-harmonic steps
   const int col = lane & 15, part = col & 1, kk = lane >> 4;
   const double2* __restrict__ Xr = a.X + ((size_t)c * a.nchan + (ok ? n : 0)) * a.NHP;
-  const double2 s4 = turn_phasor(4.0, phic);
+  const double2 s8 = turn_phasor(8.0, phic);
   // two accumulator pairs (even / odd steps): independent MFMA chains
   f64x4 d0 = {0.0, 0.0, 0.0, 0.0}, d1 = d0, d2 = d0, d3 = d0;
-  double2 xb[U];
+  double2 xb[UP];
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int k = 4 * u + kk;
+  for (int u = 0; u < UP; ++u) {
+    const int k = 4 * (2 * u + part) + kk;
     xb[u] = (ok && k <= N) ? Xr[k] : cmk(0.0, 0.0);
   }
   for (int b = 0; b < nblk; ++b) {
-    double2 xn[U];
+    double2 xn[UP];
     const bool more = b + 1 < nblk;
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int k = 4 * ((b + 1) * U + u) + kk;
+    for (int u = 0; u < UP; ++u) {
+      const int k = 4 * ((b + 1) * U + 2 * u + part) + kk;
       xn[u] = (more && ok && k <= N) ? Xr[k] : cmk(0.0, 0.0);
     }
-    double2 e = turn_phasor((double)(4 * b * U + kk), phic);
+    double2 e = turn_phasor((double)(4 * (b * U + part) + kk), phic);
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const double v = (double)(4 * (b * U + u) + kk) * iN;
-      const double v2 = v * v, v4 = v2 * v2, v8 = v4 * v4;
-      double pc = (col & 1) ? v : 1.0;
-      pc *= (col & 2) ? v2 : 1.0;
-      pc *= (col & 4) ? v4 : 1.0;
-      pc *= (col & 8) ? v8 : 1.0;
-      const double pc16 = pc * (v8 * v8);
+    for (int u = 0; u < UP; ++u) {
       const double2 W = cmul(xb[u], e);
-      const double bv = part ? W.y : W.x;
-      if (u & 1) {
-        d2 = __builtin_amdgcn_mfma_f64_16x16x4f64(pc, bv, d2, 0, 0, 0);
-        d3 = __builtin_amdgcn_mfma_f64_16x16x4f64(pc16, bv, d3, 0, 0, 0);
-      } else {
-        d0 = __builtin_amdgcn_mfma_f64_16x16x4f64(pc, bv, d0, 0, 0, 0);
-        d1 = __builtin_amdgcn_mfma_f64_16x16x4f64(pc16, bv, d1, 0, 0, 0);
+      const double recv = dpp_mov<0xB1>(part ? W.x : W.y);
+      const double bv0 = part ? recv : W.x;  // step 2u: part p of the even harmonic
+      const double bv1 = part ? W.y : recv;  // step 2u + 1
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const double v = (double)(4 * (b * U + 2 * u + h) + kk) * iN;
+        const double v2 = v * v, v4 = v2 * v2, v8 = v4 * v4;
+        double pc = (col & 1) ? v : 1.0;
+        pc *= (col & 2) ? v2 : 1.0;
+        pc *= (col & 4) ? v4 : 1.0;
+        pc *= (col & 8) ? v8 : 1.0;
+        const double pc16 = pc * (v8 * v8);
+        const double bv = h ? bv1 : bv0;
+        if (h) {
+          d2 = __builtin_amdgcn_mfma_f64_16x16x4f64(pc, bv, d2, 0, 0, 0);
+          d3 = __builtin_amdgcn_mfma_f64_16x16x4f64(pc16, bv, d3, 0, 0, 0);
+        } else {
+          d0 = __builtin_amdgcn_mfma_f64_16x16x4f64(pc, bv, d0, 0, 0, 0);
+          d1 = __builtin_amdgcn_mfma_f64_16x16x4f64(pc16, bv, d1, 0, 0, 0);
+        }
       }
-      e = cmul(e, s4);
+      e = cmul(e, s8);
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) xb[u] = xn[u];
+    for (int u = 0; u < UP; ++u) xb[u] = xn[u];
   }
   d0 += d2;
   d1 += d3;
