@@ -541,6 +541,119 @@ __device__ __forceinline__ void rfft_pair(const double2* buf, int k, double2 w, 
   Xnk = cconj(csub(E, P));
 }
 
+// Same, from the two packed values Z_k and Z_{(N-k) mod N} already loaded.
+__device__ __forceinline__ void rfft_pair_v(double2 zk, double2 znk, double2 w, double2& Xk,
+                                            double2& Xnk) {
+  const double2 zc = cconj(znk);
+  const double2 E = cscale(cadd(zk, zc), 0.5);
+  const double2 dd = csub(zk, zc);
+  const double2 O = cmk(0.5 * dd.y, -0.5 * dd.x);
+  const double2 P = cmul(w, O);
+  Xk = cadd(E, P);
+  Xnk = cconj(csub(E, P));
+}
+
+// ---------------------------------------------------------------------------
+// Register-resident 1024-point forward FFT of one packed row per wave
+// (nbin = 2048, the headline shape).  N = 16 x 16 x 4:
+//   A  lane j holds z[j + 64 m] (the coalesced row load), 16-point DFT over m
+//      in registers, twiddle W_1024^{j r}, one LDS transpose;
+//   B  lane (j0 = l & 3, r = l >> 2) takes Y_{j0 + 4 t}[r], 16-point DFT over
+//      t in registers, twiddle W_64^{j0 s};
+//   C  4-point DFT over j0 across each lane quad (two DPP radix-2 steps);
+// then Z_k goes to LDS once, in the padded order P(k) = k + 4 (k >> 8) that
+// keeps the quad-strided writes and the (k, N - k) reads of the real-FFT
+// post-processing free of bank conflicts.  Two LDS round trips per row
+// instead of the Stockham path's six.  Twiddles are exact table values
+// (W^{4a+b} = W^{4a} W^b: at most one rounding).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double2 mul_negi(double2 a) { return cmk(a.y, -a.x); }
+
+// 16-point forward DFT in place; Y[c + 4 d] ends in v[4 c + d].
+__device__ __forceinline__ void dft16(double2 (&v)[16]) {
+  constexpr double C1 = 0.92387953251128675613, S1 = 0.38268343236508977173,
+                   H = 0.70710678118654752440;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) radix4<false>(v[b], v[4 + b], v[8 + b], v[12 + b]);
+  v[5] = cmul(v[5], cmk(C1, -S1));
+  v[9] = cmul(v[9], cmk(H, -H));
+  v[13] = cmul(v[13], cmk(S1, -C1));
+  v[6] = cmul(v[6], cmk(H, -H));
+  v[10] = mul_negi(v[10]);
+  v[14] = cmul(v[14], cmk(-H, -H));
+  v[7] = cmul(v[7], cmk(S1, -C1));
+  v[11] = cmul(v[11], cmk(-H, -H));
+  v[15] = cmul(v[15], cmk(-C1, S1));
+#pragma unroll
+  for (int c = 0; c < 4; ++c) radix4<false>(v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]);
+}
+__device__ __forceinline__ constexpr int dft16_pos(int r) { return 4 * (r & 3) + (r >> 2); }
+
+// Stage twiddles, one LDS table per workgroup (read per row, not held in
+// registers across the channel loop).
+struct Fft1024Tw {
+  double2 a[3][64], b[3][64];  // W_1024^{j b}, W_1024^{4 j a}  (stage A, j = lane), b, a = 1..3
+  double2 c[3][4], d[3][4];    // W_64^{j0 b}, W_64^{4 j0 a}    (stage B, j0 = lane & 3)
+  // tw[m] = e^{-2 pi i m / 2048}
+  __device__ __forceinline__ void fill(const double2* __restrict__ tw, int t, int nt) {
+    for (int e = t; e < 3 * 64; e += nt) {
+      const int i = 1 + e / 64, j = e % 64;
+      a[i - 1][j] = tw[2 * j * i];
+      b[i - 1][j] = tw[8 * j * i];
+    }
+    for (int e = t; e < 3 * 4; e += nt) {
+      const int i = 1 + e / 4, j0 = e % 4;
+      c[i - 1][j0] = tw[32 * j0 * i];
+      d[i - 1][j0] = tw[128 * j0 * i];
+    }
+  }
+};
+__device__ __forceinline__ double2 tw_pow(int r, const double2 (&lo)[4], const double2 (&hi)[4]) {
+  const int b = r & 3, a = r >> 2;
+  if (a == 0) return lo[b];
+  if (b == 0) return hi[a];
+  return cmul(hi[a], lo[b]);
+}
+constexpr int kFftPadRow = 68;                // stage-A transpose row pitch
+constexpr int kFft1024Slots = 16 * kFftPadRow;  // >= P(1024) + 1
+__device__ __forceinline__ int fft1024_slot(int k) { return k + ((k >> 8) << 2); }
+
+// row: x[m], y[m] = packed sample j + 64 m of this lane (WaveRow<10>).
+__device__ __forceinline__ void fft1024_wave(const double (&x)[16], const double (&y)[16],
+                                             double2* buf, const Fft1024Tw& t, int lane) {
+  double2 v[16];
+#pragma unroll
+  for (int m = 0; m < 16; ++m) v[m] = cmk(x[m], y[m]);
+  double2 lo[4], hi[4];
+  lo[0] = hi[0] = cmk(1.0, 0.0);
+#pragma unroll
+  for (int i = 1; i < 4; ++i) { lo[i] = t.a[i - 1][lane]; hi[i] = t.b[i - 1][lane]; }
+  dft16(v);
+#pragma unroll
+  for (int r = 0; r < 16; ++r)
+    buf[r * kFftPadRow + lane] = r ? cmul(v[dft16_pos(r)], tw_pow(r, lo, hi)) : v[0];
+  fft_sync<true>();
+  const int j0 = lane & 3, rr = lane >> 2;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) v[q] = buf[rr * kFftPadRow + j0 + 4 * q];
+#pragma unroll
+  for (int i = 1; i < 4; ++i) { lo[i] = t.c[i - 1][j0]; hi[i] = t.d[i - 1][j0]; }
+  dft16(v);
+  fft_sync<true>();
+  const bool p = (lane & 2) != 0, q = (lane & 1) != 0;
+  const int u = (p ? 1 : 0) + (q ? 2 : 0);
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const double2 a = s ? cmul(v[dft16_pos(s)], tw_pow(s, lo, hi)) : v[0];
+    const double2 o = cmk(dpp_mov<0x4E>(a.x), dpp_mov<0x4E>(a.y));  // lane ^ 2
+    double2 b = p ? csub(o, a) : cadd(a, o);
+    if (p && q) b = mul_negi(b);
+    const double2 o2 = cmk(dpp_mov<0xB1>(b.x), dpp_mov<0xB1>(b.y));  // lane ^ 1
+    buf[rr + 16 * s + 260 * u] = q ? csub(o2, b) : cadd(b, o2);
+  }
+  fft_sync<true>();
+}
+
 // Channel walk of one wave: n = first, first + step, ... skipping masked.
 __device__ __forceinline__ int next_chan(int n, int step, int nchan, const uint8_t* mask) {
   while (n < nchan && mask && !mask[n]) n += step;

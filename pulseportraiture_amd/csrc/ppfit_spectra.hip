@@ -86,7 +86,9 @@ struct XspecCfg {
   // in the subint's global R row (too large for registers)
   static constexpr bool RREG = LOGN <= 10;
   static constexpr int WPB = RREG ? 4 : 1;
-  static constexpr int NB = N + 8;                       // row buffer slots
+  // LOGN 10: register FFT (fft1024_wave) in the padded slot order
+  static constexpr bool REGFFT = LOGN == 10;
+  static constexpr int NB = REGFFT ? kFft1024Slots : N + 8;  // row buffer slots
   static constexpr int NPI = (N / 2 + 1 + 63) / 64;      // pair iterations (k <= N/2)
   static constexpr int NRQ = RREG ? (N + 1 + WPB * 64 - 1) / (WPB * 64) : 1;  // R slots/thread
 };
@@ -100,9 +102,14 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
   constexpr int NPI = Cfg::NPI;
   constexpr int NTW = PassTw<LOGN>::SIZE;
   constexpr bool RREG = Cfg::RREG;
+  constexpr bool REGFFT = Cfg::REGFFT;
   constexpr int nthr = WPB * 64;
   __shared__ double2 bufs[WPB][Cfg::NB];
-  __shared__ double2 twl[NTW];
+  // per-pass Stockham twiddles, or the register FFT's stage tables
+  __shared__ __align__(16) unsigned char twraw[REGFFT ? sizeof(Fft1024Tw) : NTW * sizeof(double2)];
+  double2* twl = reinterpret_cast<double2*>(twraw);
+  Fft1024Tw* ftw = reinterpret_cast<Fft1024Tw*>(twraw);
+  auto bi = [](int k) { return REGFFT ? fft1024_slot(k) : k; };
   __shared__ double s_meta[4];
   __shared__ int s_act[WPB];
   extern __shared__ __align__(16) unsigned char dyn[];
@@ -121,7 +128,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
   WaveRow<LOGN> row;
   bool have = active(w);  // the registers hold (or are loading) this wave's next row
   if (have) row.load(drow0 + (size_t)w * 2 * N, lane);  // first row in flight
-  fill_pass_tw<LOGN>(twl, a.tw, tid, nthr);
+  if constexpr (REGFFT) ftw[0].fill(a.tw, tid, nthr);
+  else fill_pass_tw<LOGN>(twl, a.tw, tid, nthr);
   // nu_g (guess dedispersion reference) default: mean over fitted channels
   if (tid == 0) {
     double fs = 0.0, ws = 0.0;
@@ -184,11 +192,15 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
     };
     double2 m0k = cmk(0.0, 0.0), m0n = m0k, m1k = m0k, m1n = m0k;
     if (act) {
-      row.store(buf, drow0 + (size_t)n * 2 * N, lane);
       mload(0, m0k, m0n);
       mload(1, m1k, m1n);
-      fft_sync<true>();
-      wave_fft<LOGN>(buf, twl, lane);
+      if constexpr (REGFFT) {
+        fft1024_wave(row.x, row.y, buf, ftw[0], lane);
+      } else {
+        row.store(buf, drow0 + (size_t)n * 2 * N, lane);
+        fft_sync<true>();
+        wave_fft<LOGN>(buf, twl, lane);
+      }
     }
     // next row of this wave streams in during the spectrum pass
     if (active(n + WPB)) {
@@ -217,7 +229,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
         mload(i + 2, m1k, m1n);
         if (k <= N / 2) {
           double2 xk, xn;
-          rfft_pair<LOGN>(buf, k, tw, xk, xn);
+          rfft_pair_v(buf[bi(k)], buf[bi((N - k) & (N - 1))], tw, xk, xn);
           const int kn = N - k;
           const double p2k = cabs2(xk), p2n = cabs2(xn);
           const bool two = k < N / 2;  // k = N/2 is its own partner
@@ -234,8 +246,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
             // the pair's two slots are read and written by this lane only
             const double2 tk = cscale(cmul(xk, e), wgt);
             const double2 tn = cscale(cmul(xn, cmul(EN, cconj(e))), wgt);
-            if (two) buf[kn] = tn;  // k = 0: the N slot
-            buf[k] = tk;
+            if (two) buf[bi(kn)] = tn;  // k = 0: the N slot
+            buf[bi(k)] = tk;
           }
         }
       }
@@ -265,7 +277,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
           if (k <= N)
 #pragma unroll
             for (int v = 0; v < WPB; ++v)
-              if (s_act[v]) rq[q] = cadd(rq[q], bufs[v][k]);
+              if (s_act[v]) rq[q] = cadd(rq[q], bufs[v][bi(k)]);
         }
       } else {
         if (s_act[0])
