@@ -440,8 +440,9 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
       return r;
     if (taylor) {
       if (int r = timed(ctx, PPF_K_MOMENTS, [&] {
-            hipLaunchKernelGGL(k_moments, dim3(nc, (nchan + 8 * kWaves - 1) / (8 * kWaves)),
-                               dim3(kBlock), 0, ctx->stream, fa);
+            const dim3 g(nc, (nchan + 8 * kWaves - 1) / (8 * kWaves));
+            // steps in flight: 8 / 16 / 32 time the same (r01 sweep): not load-latency bound
+            hipLaunchKernelGGL(k_moments<16>, g, dim3(kBlock), 0, ctx->stream, fa);
           }))
         return r;
       if (int r = timed(ctx, PPF_K_FIT_TAYLOR, [&] {

@@ -321,6 +321,7 @@ __global__ void k_accum_reduce(const double2* partial, double2* accum, int nspli
 __global__ void k_guess(FitArgs a);
 __global__ void k_model_mean(const double2* M, double2* Mmean, int nchan, int NHP);
 __global__ void k_fit_taylor(FitArgs a);
+template <int U>
 __global__ void k_moments(FitArgs a);
 __global__ void k_selftest(int* fails);
 template <bool SCAT> __global__ void k_solve(FitArgs a);

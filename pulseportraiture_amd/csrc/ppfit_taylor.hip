@@ -179,6 +179,7 @@ __device__ void moments_from_X(const FitArgs& a, const Meta& m, int c, int s, in
 // full occupancy.  Block (c, y): wave w takes channels 8 (4 y + w) .. + 7
 // (masked channels idle in their lane).
 // ---------------------------------------------------------------------------
+template <int U>
 __global__ __launch_bounds__(kBlock) void k_moments(FitArgs a) {
   const int c = blockIdx.x, s = a.sub0 + c;
   if (!fused_taylor(a, s)) return;
@@ -190,8 +191,10 @@ __global__ __launch_bounds__(kBlock) void k_moments(FitArgs a) {
   const bool ok = n < a.nchan && (!a.mask || a.mask[(size_t)s * a.nchan + n]);
   const double phic = ok ? phase_frac(st.xc[0], a.freqs[(size_t)s * a.nchan + n], st.refs, a.P[s])
                          : 0.0;
-  moment_tile<16>(a, c, 0, n, ok, phic);
+  moment_tile<U>(a, c, 0, n, ok, phic);
 }
+
+template __global__ void k_moments<16>(FitArgs);
 
 // ---------------------------------------------------------------------------
 // k_fit_taylor: one workgroup per phase-family subint, the whole fit:
