@@ -6,19 +6,17 @@
 //   C_n(phi_n)   = Re  sum_k X_nk e^{2 pi i k phi_n}        (pptoaslib.py:431)
 //   dC_n/dphi_n  ∝ Im  sum_k k X_nk e^{2 pi i k phi_n}      (pptoaslib.py:437-449)
 //   d2C_n/dphi_n2 ∝ Re sum_k k^2 X_nk e^{2 pi i k phi_n}    (pptoaslib.py:451-461)
-// with X_nk = D_nk conj(M_nk).  Instead of writing X (16 B per cell) and
-// re-reading it on every trust-region evaluation, k_moments transforms the
-// data rows once more and reduces each channel to kMT Taylor moments about a
-// centre phi_c,n:
+// with X_nk = D_nk conj(M_nk).  Instead of re-reading X (16 B per cell) on
+// every trust-region evaluation, k_moments reads it once and reduces each
+// channel to kMT Taylor moments about a centre phi_c,n:
 //   T_nm = sum_k v_k^m X_nk e^{2 pi i k phi_c,n},   v_k = k / N,
 // so that any later evaluation within |2 pi N (phi_n - phi_c,n)| <= kTaylorY
 // is a kMTerm-term series (taylor_cells in ppfit_fit.hip) accurate to the
-// fp64 rounding of the exact sums.  k_solve_taylor runs scipy's trust-ncg
-// on those series; a proposal outside the radius of both stored centres
-// parks the subint with its state saved, the host recentres it with one
-// more k_moments pass over its data, and the solve resumes.  Per subint the
-// data portrait is read twice (k_data_xspec, k_moments) and nothing of size
-// nchan x nharm is written.
+// fp64 rounding of the exact sums.  k_fit_taylor runs scipy's trust-ncg on
+// those series; a proposal outside the radius of both stored centres gets a
+// new centre (one more pass over the subint's X, moments_from_X) first.  Per
+// subint X is written once (k_data_xspec) and read once (k_moments), plus
+// once per recentring.
 #include "ppfit_kernels.hpp"
 
 namespace ppf {
