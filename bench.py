@@ -4,11 +4,13 @@
 One step = the whole hot path over one batch of synthetic subints already
 resident in HBM: per-channel rfft + noise + cross-spectrum (k_data_xspec),
 the get_TOAs initial guess (k_guess: dedispersed average, brute force Ns=100,
-Nelder-Mead), the trust-ncg fit (k_solve) and the post-fit (k_post:
-zero-covariance frequency, phi at nu_out, Woodbury covariance, snr, chi2),
-then the per-TOA results copied to the host.  Data: synthetic portraits from
-example.gmodel with injected phi/DM and sigma=1.5 Philox noise, generated on
-the device before timing.
+Nelder-Mead), Taylor moments of the cross-spectrum (k_moments) and the
+trust-ncg fit on them (k_fit_taylor) -- or, for scattering fits, the exact
+sweeps of k_solve -- and the post-fit (k_post: zero-covariance frequency,
+phi at nu_out, Woodbury covariance, snr, chi2), then the per-TOA results
+copied to the host.  Data: synthetic portraits from example.gmodel with
+injected phi/DM and sigma=1.5 Philox noise, generated on the device before
+timing.
 
 N>1: launched by torch.distributed.run, one rank per GPU; each rank fits its
 own nsub subints (weak scaling, no collective on the fit path).  value =

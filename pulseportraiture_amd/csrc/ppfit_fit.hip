@@ -184,7 +184,7 @@ __device__ __forceinline__ void cells_phase(const double2* __restrict__ Xr, int 
 __device__ __forceinline__ void cells_scat(const double2* __restrict__ Xr,
                                            const double2* __restrict__ Mr, int J, int h,
                                            double phif, double taun, double* acc) {
-  constexpr int U = 2;
+  constexpr int U = 2;  // 4 in flight: 256 VGPRs, one wave per SIMD, no faster (r01)
   const double2 step = turn_phasor(8.0, phif);
   const double itau = 1.0 / taun;
   const double w0 = kTwoPi * taun;
