@@ -1419,8 +1419,11 @@ __device__ void post_subint(const FitArgs& a, int c, int s, unsigned char* dyn, 
   }
 }
 
+// Phase-family post-fit: capped at 128 VGPRs for four waves per SIMD (its
+// serial thread-0 sections are latency-bound; 1.16 -> 1.00 ms at config 2
+// despite the spills).  The scattering variant keeps its registers.
 template <bool SCAT>
-__global__ __launch_bounds__(kBlock) void k_post(FitArgs a) {
+__global__ __launch_bounds__(kBlock, SCAT ? 1 : 4) void k_post(FitArgs a) {
   extern __shared__ __align__(16) unsigned char dyn[];
   __shared__ PostShared sh;
   const int c = blockIdx.x, s = a.sub0 + c;
