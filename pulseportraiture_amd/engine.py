@@ -43,7 +43,7 @@ def _dev_u8(x, dev):
         return None
     if isinstance(x, torch.Tensor):
         return x.to(device=dev, dtype=torch.uint8).contiguous()
-    return torch.as_tensor(np.ascontiguousarray(x, dtype=np.uint8), device=dev)
+    return torch.as_tensor(np.array(x, dtype=np.uint8), device=dev)  # copy: inputs may be read-only views
 
 
 def _ptr(t):

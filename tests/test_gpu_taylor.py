@@ -154,3 +154,31 @@ def test_taylor_vs_oracle_headline_shape(eng):
         assert abs(out["params"][i][1] - ref.DM) <= 1e-3 * ref.DM_err
         assert out["param_errs"][i][0] == pytest.approx(ref.phi_err, rel=1e-6)
         assert out["red_chi2"][i] == pytest.approx(ref.red_chi2, rel=1e-9)
+
+
+def test_taylor_vs_oracle_headline_masked(eng):
+    """64 x 2048 (the register-FFT data pass) with masked channels against the
+    oracle fitting only the unmasked channels, as get_TOAs does with its
+    zero-weight channels removed."""
+    nsub, nchan = 3, 64
+    w = synth.make_workload(nsub, nchan, 2048, seed=91)
+    data = synth.workload_data_host(w)
+    mask = np.ones((nsub, nchan), np.uint8)
+    mask[0, ::4] = 0
+    mask[1, 32:] = 0
+    mask[2, [0, 1, 62, 63]] = 0
+    nu = O.guess_fit_freq(w.freqs)
+    out = _np(eng.fit_batch(data, w.model, w.freqs, w.P, [0.0, w.DM0, 0, 0, 0], [1, 1, 0, 0, 0],
+                            nu_fit=[nu, nu, nu], chan_mask=mask, guess=True))
+    for i in range(nsub):
+        ok = mask[i].astype(bool)
+        errs = O.get_noise_PS(data[i][ok], chans=True)
+        ref = O.fit_portrait_full(data[i][ok], w.model[ok], list(out["init_used"][i]), w.P,
+                                  w.freqs[ok], [nu] * 3, [None] * 3, errs, [1, 1, 0, 0, 0],
+                                  log10_tau=False)
+        assert out["status"][i] == ref.return_code
+        assert abs(out["params"][i][0] - ref.phi) <= 1e-3 * ref.phi_err
+        assert abs(out["params"][i][1] - ref.DM) <= 1e-3 * ref.DM_err
+        assert out["param_errs"][i][0] == pytest.approx(ref.phi_err, rel=1e-6)
+        assert out["red_chi2"][i] == pytest.approx(ref.red_chi2, rel=1e-9)
+        assert np.all(out["scales"][i][~ok] == 0.0)
