@@ -122,6 +122,8 @@ struct GuessShared {
   double x0, x, fx;
   double out[8];
   double bf[kBlock];       // brute force: partial sums per (half, grid point)
+  double2 fb[kBlock / 2];  // folded grid: b_j = sum_{k = j mod L} (-1)^k rm_k
+  double2 fw[kBlock / 2];  //              w_m = e^{2 pi i m / L}
   double ev[2][kWaves];    // Nelder-Mead: per-wave partials, double-buffered
 };
 
@@ -196,12 +198,48 @@ __device__ inline void guess_search(const double2* rm, int NH, double ie2, int N
   const int kmid = (NH + 1) / 2;
   double bv = NAN;
   int bi = 0x7fffffff;
+  // On the get_TOAs grid (lo, hi) = (-0.5, 0.5) every grid phase is
+  // -1/2 + g / L, L = Ns - 1, so f(phi_g) = Re sum_j b_j w^{j g} with the
+  // spectrum folded mod L: an L-point DFT instead of Ns x NH phasor terms.
+  // The end points phi = -0.5 and 0.5 get the same folded sum (w^0 and w^L):
+  // their direct sums were already bitwise equal (turn_phasor is exact at
+  // half turns), so argmin's tie rule still picks g = 0.  Every grid point
+  // takes the folded path: a direct sum on any lane would hold its wave.
+  const int L = Ns - 1;
+  const bool fold = lo == -0.5 && hi == 0.5 && L >= 2 && L <= GP && NH > 2 * L;
+  if (fold) {
+    if (tid < L) {
+      double2 b = cmk(0.0, 0.0);
+      for (int k = tid; k < NH; k += L) {
+        const double2 r = rm[k];
+        b = (k & 1) ? csub(b, r) : cadd(b, r);
+      }
+      gs.fb[tid] = b;
+      double sn, cs;
+      sincospi(2.0 * (double)tid / (double)L, &sn, &cs);
+      gs.fw[tid] = cmk(cs, sn);
+    }
+    __syncthreads();
+  }
   for (int g0 = 0; g0 < Ns; g0 += GP) {
     const int g = g0 + gl;
     double part = 0.0;
     if (g < Ns) {
-      const double ph = (g == Ns - 1) ? hi : __dadd_rn(__dmul_rn((double)g, step), lo);
-      part = half ? row_eval_phase(rm, kmid, NH, ph) : row_eval_phase(rm, 0, kmid, ph);
+      if (fold) {
+        const int jm = (L + 1) / 2;
+        const int j0 = half ? jm : 0, j1 = half ? L : jm;
+        int mi = (j0 * g) % L;
+        for (int j = j0; j < j1; ++j) {
+          const double2 b = gs.fb[j], wv = gs.fw[mi];
+          part = fma(b.x, wv.x, part);
+          part = fma(-b.y, wv.y, part);
+          mi += g;
+          if (mi >= L) mi -= L;
+        }
+      } else {
+        const double ph = (g == Ns - 1) ? hi : __dadd_rn(__dmul_rn((double)g, step), lo);
+        part = half ? row_eval_phase(rm, kmid, NH, ph) : row_eval_phase(rm, 0, kmid, ph);
+      }
     }
     gs.bf[tid] = part;
     __syncthreads();
