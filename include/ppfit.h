@@ -32,7 +32,7 @@
  *    trust-ncg codes (0 gradient small / NaN, 1 maxiter, 2 no predicted
  *    reduction, 3 linalg error), as returned by the reference's
  *    results.status (pptoaslib.py:1018).
- *  - nbin must be a power of two in [16, 8192]; nchan <= PPF_MAX_NCHAN.
+ *  - nbin must be a power of two in [64, 8192]; nchan <= PPF_MAX_NCHAN.
  */
 #ifndef PPFIT_H
 #define PPFIT_H
@@ -101,20 +101,30 @@ int ppf_phase_profile(ppf_ctx* ctx, int32_t enable, uint64_t* out);
 /* ---------------------------------------------------------------------- */
 /* Batched wideband fit: fit_portrait_full over nsub subints.              */
 /* ---------------------------------------------------------------------- */
-#define PPF_METHOD_TRUST_NCG 0
+/* minimize() method of fit_portrait_full (pptoaslib.py:995-1014)          */
+#define PPF_METHOD_TRUST_NCG 0   /* scipy trust-ncg, gtol = -1 (the default)  */
+#define PPF_METHOD_TNC 1         /* scipy TNC with bounds, xtol 1e-10, minfev */
+#define PPF_METHOD_NEWTON_CG 2   /* scipy Newton-CG, xtol = -1, maxiter 2000   */
 
 /* Phase-family fits (tau = 0 and not fitted) evaluate the objective from
  * per-channel Taylor moments of the cross-spectrum (no nchan x nharm
  * workspace).  PPF_SOLVE_EXACT forces the exact cross-spectrum sweeps
- * instead (same results to rounding; used to cross-check the two).       */
+ * instead (same results to rounding; used to cross-check the two).
+ * PPF_SOLVE_EVAL evaluates f, g, H and the post-fit at init without any
+ * solver step (status 1, nfev 1): the objective-kernel parity hook for
+ * fit_portrait_full_function{,_deriv,_2deriv} (pptoaslib.py:525-643).
+ * PPF_GUESS_DIRECT takes the brute-force grid of the initial guess by
+ * direct sums instead of the folded L-point DFT.                          */
 #define PPF_SOLVE_EXACT 1
+#define PPF_SOLVE_EVAL 2
+#define PPF_GUESS_DIRECT 4
 
 typedef struct {
   int32_t nsub, nchan, nbin, nmodel;
   int32_t fit_flags[5];   /* phi, DM, GM, tau, alpha (pptoaslib.py:928)     */
   int32_t log10_tau;      /* fit log10(tau) instead of tau                 */
   int32_t option;         /* get_nu_zeros option (pptoaslib.py:733)        */
-  int32_t method;         /* PPF_METHOD_TRUST_NCG                           */
+  int32_t method;         /* PPF_METHOD_*                                   */
   int32_t is_toa;         /* pptoaslib.py:1048-1050                         */
   int32_t guess;          /* 1: in-kernel initial phase guess (pptoas.py:420-456) */
   int32_t guess_Ns;       /* opt.brute grid size (100 in pptoas, nbin in ppalign) */
@@ -124,8 +134,8 @@ typedef struct {
   const double* model;      /* [nmodel][nchan][nbin]                        */
   const int32_t* model_idx; /* [nsub] or NULL (all 0)                       */
   const double* freqs;      /* [nsub][nchan] MHz                            */
-  const double* errs;       /* [nsub][nchan] time-domain sigma, or NULL:
-                               estimated as get_noise_PS (pplib.py:2227)    */
+  const double* errs;       /* [nsub][nchan] time-domain sigma; NULL or a NaN
+                               entry: estimated as get_noise_PS (pplib.py:2227) */
   const uint8_t* chan_mask; /* [nsub][nchan] 1 = fit channel, or NULL       */
   const double* weights;    /* [nsub][nchan] guess-average weights or NULL  */
   const double* P;          /* [nsub] period, s                             */
@@ -136,6 +146,9 @@ typedef struct {
                                mean freq (pptoas) ; NULL -> NaN             */
   const double* guess_tau;  /* [nsub] linear tau [rot] at nu_fit_tau applied
                                to the guess template, or NULL (0)           */
+  const double* bounds;     /* HOST pointer, [5][2] (low, high) per parameter
+                               for the whole batch, NaN = None; read by
+                               PPF_METHOD_TNC only (NULL = all None)        */
 } ppf_fit_desc;
 
 typedef struct {
@@ -156,6 +169,8 @@ typedef struct {
   double* cov_nosc;     /* [nsub][5][5] or NULL: inv(0.5 H) of the curvature
                            without amplitude terms at the output params
                            (legacy pplib.fit_portrait errors, pplib.py:2184-2190) */
+  double* grad;         /* [nsub][5] or NULL: gradient at the final point (jac) */
+  double* hess;         /* [nsub][5][5] or NULL: Hessian at the final point     */
 } ppf_fit_result;
 
 int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* desc,

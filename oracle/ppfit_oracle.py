@@ -215,13 +215,27 @@ def channel_terms(params, dFT, mFT, errs_FT, P, freqs, nu_DM, nu_GM, nu_tau,
     ph = phase_shifts(phi, DM, GM, freqs, nu_DM, nu_GM, P)
     dph = phase_shift_jacobian(freqs, nu_DM, nu_GM, P)
     taus = scattering_times(tau, alpha, freqs, nu_tau)
-    dts, d2ts = _tau_jacobians(tau, freqs, nu_tau, log10_tau, taus)
-    B = scattering_portrait_FT(taus, nbin)
-    dB, d2B = _scat_FT_derivs(taus, dts, d2ts, B)
     W = dFT * np.conj(mFT) * np.exp(2.0j * np.pi * np.outer(ph, k))
     m2 = np.abs(mFT) ** 2
     w2 = errs_FT ** 2
     tpk = 2.0j * np.pi * k
+    if not taus.sum():
+        # tau = 0: B = 1 and every tau/alpha derivative of B vanishes
+        # (pptoaslib.py:318-356 return zeros), so only the phase family is left
+        C = np.real(W.sum(-1))
+        C1 = np.real((tpk * W).sum(-1))
+        C2 = np.real((tpk ** 2 * W).sum(-1))
+        S = m2.sum(-1)
+        dC = np.zeros((5, nchan))
+        dC[:3] = C1 * dph
+        d2C = np.zeros((5, 5, nchan))
+        d2C[:3, :3] = C2 * dph[:, None] * dph[None]
+        z5 = np.zeros((5, nchan))
+        return Bunch(C=C / w2, dC=dC / w2, d2C=d2C / w2, S=S / w2, dS=z5,
+                     d2S=np.zeros((5, 5, nchan)), taus=taus)
+    dts, d2ts = _tau_jacobians(tau, freqs, nu_tau, log10_tau, taus)
+    B = scattering_portrait_FT(taus, nbin)
+    dB, d2B = _scat_FT_derivs(taus, dts, d2ts, B)
     C = np.real(np.sum(W * np.conj(B), -1))
     C1 = np.real(np.sum(tpk * W * np.conj(B), -1))
     C2 = np.real(np.sum(tpk ** 2 * W * np.conj(B), -1))
@@ -654,17 +668,22 @@ def fit_portrait(data, model, init_params, P, freqs, nu_fit=None, nu_out=None,
 # L4 per-subint driver steps (pptoas.py:383-530, ppalign.py:160-208)
 # ---------------------------------------------------------------------------
 def pptoas_guess(portx, modelx, freqsx, weightsx, DM_guess, P, nu_fit_DM,
-                 Ns=100, nu_rot=None, wrap=True, model_prof=None):
+                 Ns=100, nu_rot=None, wrap=True, model_prof=None, tau_guess=0.0):
     """Initial phase guess of get_TOAs, pptoas.py:420-456.
 
     Dedisperse at nu_rot (default: mean frequency), average with channel
-    weights, brute-force FFTFIT against the mean model profile, then move the
-    phase to nu_fit_DM.
+    weights, brute-force FFTFIT against the mean model profile (scattered by
+    tau_guess [rot] when fitting scattering, pptoas.py:441-444), then move
+    the phase to nu_fit_DM.
     """
     nu_mean = freqsx.mean() if nu_rot is None else nu_rot
     rot = rotate_data(portx, 0.0, DM_guess, P, freqsx, nu_mean)
     prof = np.average(rot, axis=0, weights=weightsx)
     mp = modelx.mean(axis=0) if model_prof is None else model_prof
+    if tau_guess:
+        nbin = len(mp)
+        mp = np.fft.irfft(scattering_portrait_FT(np.array([tau_guess]), nbin)[0] *
+                          np.fft.rfft(mp))
     phi = fit_phase_shift(prof, mp, Ns=Ns).phase
     if not wrap:
         return phi
@@ -672,12 +691,18 @@ def pptoas_guess(portx, modelx, freqsx, weightsx, DM_guess, P, nu_fit_DM,
 
 
 def fit_subint_pptoas(portx, modelx, freqsx, weightsx, errs, SNRsx, P, DM_stored,
-                      fit_flags=(1, 1, 0, 0, 0), Ns=100, log10_tau=False):
-    """One TOA of get_TOAs (guess + fit), pptoas.py:383-488 (no scattering)."""
+                      fit_flags=(1, 1, 0, 0, 0), Ns=100, log10_tau=False,
+                      tau_guess=0.0, alpha_guess=0.0):
+    """One TOA of get_TOAs (guess + fit), pptoas.py:383-488.  For scattering
+    fits tau_guess [rot] at nu_fit scatters the guess template and starts the
+    fit (log10 of it with log10_tau; 1/nbin when 0, pptoas.py:441-450)."""
     nu_fit = guess_fit_freq(freqsx, SNRsx)
     phi_guess = pptoas_guess(portx, modelx, freqsx, weightsx, DM_stored, P,
-                             nu_fit, Ns)
-    init = [phi_guess, DM_stored, 0.0, 0.0, 0.0]
+                             nu_fit, Ns, tau_guess=tau_guess)
+    tau0 = tau_guess
+    if log10_tau:
+        tau0 = np.log10(tau0 if tau0 else 1.0 / portx.shape[-1])
+    init = [phi_guess, DM_stored, 0.0, tau0, alpha_guess]
     res = fit_portrait_full(portx, modelx, init, P, freqsx,
                             [nu_fit, nu_fit, nu_fit], [None, None, None], errs,
                             list(fit_flags), log10_tau=log10_tau, option=0)

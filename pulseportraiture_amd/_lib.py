@@ -12,10 +12,16 @@ LIB_PATH = os.path.join(HERE, "libppfit.so")
 
 PPF_OK = 0
 PPF_METHOD_TRUST_NCG = 0
+PPF_METHOD_TNC = 1
+PPF_METHOD_NEWTON_CG = 2
+METHODS = {"trust-ncg": PPF_METHOD_TRUST_NCG, "TNC": PPF_METHOD_TNC,
+           "Newton-CG": PPF_METHOD_NEWTON_CG}
 KERNEL_IDS = {"model_fft": 0, "data_xspec": 1, "solve": 2, "phase_shift": 3,
               "rotate": 4, "rot_accum": 5, "synth": 6, "irfft": 7, "noise": 8,
               "guess": 9, "post": 10, "fit_taylor": 11, "moments": 12}
 PPF_SOLVE_EXACT = 1
+PPF_SOLVE_EVAL = 2
+PPF_GUESS_DIRECT = 4
 PPF_SELFTEST_N = 10
 PPF_PHASE_N = 16
 
@@ -34,7 +40,8 @@ class FitDesc(ctypes.Structure):
                 ("data", _dp), ("model", _dp), ("model_idx", _dp),
                 ("freqs", _dp), ("errs", _dp), ("chan_mask", _dp),
                 ("weights", _dp), ("P", _dp), ("init", _dp), ("nu_fit", _dp),
-                ("nu_out", _dp), ("guess_nu", _dp), ("guess_tau", _dp)]
+                ("nu_out", _dp), ("guess_nu", _dp), ("guess_tau", _dp),
+                ("bounds", _dp)]
 
 
 class FitResult(ctypes.Structure):
@@ -43,7 +50,8 @@ class FitResult(ctypes.Structure):
                 ("cov", _dp), ("scales", _dp), ("scale_errs", _dp),
                 ("channel_snrs", _dp), ("chi2", _dp), ("red_chi2", _dp),
                 ("snr", _dp), ("nfev", _dp), ("status", _dp),
-                ("init_used", _dp), ("fun", _dp), ("cov_nosc", _dp)]
+                ("init_used", _dp), ("fun", _dp), ("cov_nosc", _dp),
+                ("grad", _dp), ("hess", _dp)]
 
 
 EXPORTS = {

@@ -276,6 +276,8 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   if (d->nmodel <= 0) return fail(ctx, PPF_ERR_INVALID, "nmodel must be >= 1");
   if (d->method != PPF_METHOD_TRUST_NCG)
     return fail(ctx, PPF_ERR_UNSUPPORTED, "Method %d is not implemented.", d->method);
+  if (d->solver_flags & ~(PPF_SOLVE_EXACT | PPF_SOLVE_EVAL | PPF_GUESS_DIRECT))
+    return fail(ctx, PPF_ERR_INVALID, "unknown solver_flags bits 0x%x", d->solver_flags);
   if (!d->data || !d->model || !d->freqs || !d->P || !d->init || !d->nu_fit || !d->nu_out)
     return fail(ctx, PPF_ERR_INVALID, "missing required input pointer");
   if (!o->params || !o->param_errs || !o->nu_out || !o->cov || !o->scales || !o->scale_errs ||
@@ -374,6 +376,10 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   fa.guess = d->guess;
   fa.Ns = d->guess_Ns;
   fa.guess_wrap = d->guess_wrap;
+  fa.solver_flags = d->solver_flags;
+  fa.method = d->method;
+  for (int i = 0; i < 5; ++i)
+    for (int j = 0; j < 2; ++j) fa.bounds[i][j] = d->bounds ? d->bounds[2 * i + j] : NAN;
   fa.X = sa.X;
   fa.R = sa.R;
   fa.M = M;
@@ -413,6 +419,8 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   fa.o_init_used = o->init_used;
   fa.o_fun = o->fun;
   fa.o_cov_nosc = o->cov_nosc;
+  fa.o_grad = o->grad;
+  fa.o_hess = o->hess;
 
   const size_t lds_meta = align256((size_t)nchan * (5 * sizeof(double) + sizeof(int)));
   const size_t lds_guess = (size_t)NHP * sizeof(double2);

@@ -728,7 +728,8 @@ __device__ void guess_subint(const FitArgs& a, int c, int s, unsigned char* dyn,
   // err = get_noise(rot_prof) * sqrt(nbin/2), pplib.py:2076-2080
   const double noise = sqrt(pno / (double)a.nbin / (double)(a.NH - a.kc));
   const double err2 = noise * noise * (0.5 * (double)a.nbin);
-  guess_search(rm, a.NH, 1.0 / err2, a.Ns, -0.5, 0.5, gs, a.ptime ? a.ptime + 10 : nullptr);
+  guess_search(rm, a.NH, 1.0 / err2, a.Ns, -0.5, 0.5, gs, !(a.solver_flags & PPF_GUESS_DIRECT),
+               a.ptime ? a.ptime + 10 : nullptr);
   if (tid == 0) {
     double nug = a.guess_nu ? a.guess_nu[s] : NAN;
     if (isnan(nug)) nug = fmean;
@@ -840,6 +841,15 @@ __device__ __forceinline__ double steihaug(double f, double g, const double (&Hr
   return z;
 }
 
+// scipy's result jac (and the Hessian) at the final point: lane i < 5 of
+// wave 0 holds g_i and row i of H
+__device__ __forceinline__ void store_grad_hess(const FitArgs& a, int s, int lane, bool ok,
+                                                double g, const double (&Hrow)[5]) {
+  if (a.o_grad) a.o_grad[(size_t)s * 5 + lane] = ok ? g : NAN;
+  if (a.o_hess)
+    for (int j = 0; j < 5; ++j) a.o_hess[(size_t)s * 25 + lane * 5 + j] = ok ? Hrow[j] : NAN;
+}
+
 struct SolveShared {
   double x[5], xp[5];
   double out[48];
@@ -883,8 +893,13 @@ __global__ __launch_bounds__(kBlock) void k_solve(FitArgs a) {
       load_fgh(f, g, Hrow);
       xl = lane < 5 ? sh.x[lane] : 0.0;
       nfev = 1;
+      if (a.solver_flags & PPF_SOLVE_EVAL) {  // objective at init only
+        status = 1;
+        if (lane == 0) sh.done = 1;
+      }
     }
   }
+  __syncthreads();
   while (!sh.done) {
     if (tid < 64) {
       const double jm = sqrt(dot8(g, g));
@@ -934,6 +949,7 @@ __global__ __launch_bounds__(kBlock) void k_solve(FitArgs a) {
     __syncthreads();
   }
   if (tid < 5) st.x[tid] = sh.x[tid];
+  if (tid < 5) store_grad_hess(a, s, lane, m.nok > 0, g, Hrow);
   if (tid == 0) {
     st.fun = m.nok ? f : NAN;
     st.nfev = m.nok ? nfev : 0;

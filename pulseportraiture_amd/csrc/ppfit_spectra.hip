@@ -256,8 +256,9 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
       pn = wave_sum(pn);
       pd = wave_sum(pd);
       if (lane == 0) {
-        const double sig = a.errs ? a.errs[(size_t)s * nchan + n]
-                                  : sqrt(pn / (double)(2 * N) / (double)(NH - a.kc));
+        // errs NULL or NaN entry: get_noise_PS of the row (pplib.py:2227-2253)
+        double sig = a.errs ? a.errs[(size_t)s * nchan + n] : NAN;
+        if (isnan(sig)) sig = sqrt(pn / (double)(2 * N) / (double)(NH - a.kc));
         a.sig[(size_t)c * nchan + n] = sig;
         a.dsum[(size_t)c * nchan + n] = pd;
       }

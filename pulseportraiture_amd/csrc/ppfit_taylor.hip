@@ -309,9 +309,14 @@ __global__ __launch_bounds__(kBlock) void k_fit_taylor(FitArgs a) {
       load_fgh(f, g, Hrow);
       xl = lane < 5 ? sh.x[lane] : 0.0;
       nfev = 1;
+      if (a.solver_flags & PPF_SOLVE_EVAL) {  // objective at init only
+        status = 1;
+        if (lane == 0) sh.done = 1;
+      }
     }
     if (tid == 0) sh.tslot = q;
   }
+  __syncthreads();
   while (!sh.done) {
     if (tid < 64) {
       const double jm = sqrt(dot8(g, g));
@@ -365,6 +370,7 @@ __global__ __launch_bounds__(kBlock) void k_fit_taylor(FitArgs a) {
     __syncthreads();
   }
   if (tid < 5) st.x[tid] = sh.x[tid];
+  if (tid < 5) store_grad_hess(a, s, lane, m.nok > 0, g, Hrow);
   if (tid == 0) {
     st.fun = m.nok ? f : NAN;
     st.nfev = m.nok ? nfev : 0;

@@ -148,15 +148,24 @@ class Engine:
                   nu_out=None, errs=None, chan_mask=None, weights=None,
                   model_idx=None, log10_tau=False, option=0, is_toa=True,
                   guess=False, guess_Ns=100, guess_wrap=True, guess_nu=None,
-                  guess_tau=None, exact=False):
+                  guess_tau=None, exact=False, method="trust-ncg", bounds=None,
+                  eval_only=False, guess_direct=False):
         """fit_portrait_full over a batch (pptoaslib.py:928-1096).
 
         data [nsub, nchan, nbin]; model [nmodel, nchan, nbin] (or [nchan, nbin]);
         freqs [nsub, nchan] or [nchan]; P [nsub] or scalar; init [nsub, 5] or [5].
+        errs: time-domain sigma per channel; None or NaN entries are estimated
+        on the device as get_noise_PS (pplib.py:2227-2253).
         exact=True forces the exact cross-spectrum sweeps for phase-family
         fits (default: per-channel Taylor moments, ppfit_taylor.hip).
+        method: 'trust-ncg' | 'TNC' | 'Newton-CG' (pptoaslib.py:995-1014);
+        bounds: 5 (low, high) pairs, None = unbounded (TNC only).
+        eval_only: f, g, H and the post-fit at init, no solver step.
+        guess_direct: brute-force guess grid by direct sums (no folded DFT).
         Returns a dict of device tensors.
         """
+        if method not in _lib.METHODS:
+            raise PPFitError("Method '%s' is not implemented." % method)
         dev = self.device
         d = _dev_f64(data, dev)
         if d.dim() == 2:
@@ -185,12 +194,19 @@ class Engine:
             desc.fit_flags[i] = int(bool(fit_flags[i]))
         desc.log10_tau = int(bool(log10_tau))
         desc.option = int(option)
-        desc.method = _lib.PPF_METHOD_TRUST_NCG
+        desc.method = _lib.METHODS[method]
         desc.is_toa = int(bool(is_toa))
         desc.guess = int(bool(guess))
         desc.guess_Ns = int(guess_Ns)
         desc.guess_wrap = int(bool(guess_wrap))
-        desc.solver_flags = _lib.PPF_SOLVE_EXACT if exact else 0
+        desc.solver_flags = ((_lib.PPF_SOLVE_EXACT if exact else 0) |
+                             (_lib.PPF_SOLVE_EVAL if eval_only else 0) |
+                             (_lib.PPF_GUESS_DIRECT if guess_direct else 0))
+        bnd = None
+        if bounds is not None:
+            bnd = (ctypes.c_double * 10)(*[
+                np.nan if v is None else float(v) for b in bounds for v in (list(b) + [None, None])[:2]])
+        desc.bounds = ctypes.cast(bnd, ctypes.c_void_p) if bnd is not None else None
         keep = dict(d=d, m=m, fr=fr, P=Pt, it=it, nf=nf, no=no, er=er, mk=mk, wt=wt,
                     mi=mi, gn=gn, gt=gt)
         desc.data, desc.model, desc.model_idx = _ptr(d), _ptr(m), _ptr(mi)
@@ -212,11 +228,13 @@ class Engine:
                    status=torch.empty(nsub, dtype=torch.int32, device=dev),
                    init_used=torch.empty(nsub, 5, **f64),
                    fun=torch.empty(nsub, **f64),
-                   cov_nosc=torch.empty(nsub, 5, 5, **f64))
+                   cov_nosc=torch.empty(nsub, 5, 5, **f64),
+                   grad=torch.empty(nsub, 5, **f64),
+                   hess=torch.empty(nsub, 5, 5, **f64))
         res = _lib.FitResult()
         for k in ["params", "param_errs", "nu_out", "cov", "scales", "scale_errs",
                   "channel_snrs", "chi2", "red_chi2", "snr", "nfev", "status",
-                  "init_used", "fun", "cov_nosc"]:
+                  "init_used", "fun", "cov_nosc", "grad", "hess"]:
             setattr(res, k, _ptr(out[k]))
         self._chk(self.lib.ppf_fit_portrait_batch(self.ctx, ctypes.byref(desc),
                                                   ctypes.byref(res)))

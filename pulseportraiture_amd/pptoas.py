@@ -133,6 +133,7 @@ class GetTOAs:
             already_warned = True
         self.scat_guess = scat_guess
         self.DM0, self.bary = DM0, bary
+        self._fit_flags_prev = None  # the reference's loop-carried fit_flags
         start = time.time()
         datafiles = self.datafiles if datafile is None else [datafile]
         for iarch, datafile in enumerate(datafiles):
@@ -154,7 +155,7 @@ class GetTOAs:
             name = datafile if isinstance(datafile, str) else data.filename
             self._archive_toas(name, data, nu_refs, nu_fits, fit_scat, log10_tau,
                                scat_guess, print_phase, print_flux, print_parangle,
-                               addtnl_toa_flags, method, quiet, already_warned)
+                               addtnl_toa_flags, method, bounds, quiet, already_warned)
         tot = time.time() - start
         if not quiet and len(self.ok_isubs):
             n = np.array([len(x) for x in self.ok_isubs]).sum()
@@ -163,7 +164,7 @@ class GetTOAs:
 
     def _archive_toas(self, datafile, data, nu_ref_tuple, nu_fit_tuple, fit_scat, log10_tau,
                       scat_guess, print_phase, print_flux, print_parangle, addtnl_toa_flags,
-                      method, quiet, already_warned):
+                      method, bounds, quiet, already_warned):
         nsub, nchan, nbin = data.nsub, data.nchan, data.nbin
         obs = DataBunch(telescope=data.telescope, backend=data.backend, frontend=data.frontend)
         DM_stored = data.DM
@@ -219,14 +220,29 @@ class GetTOAs:
                         tau_g = nbin ** -1
                     tau_g = np.log10(tau_g)
             init[isub] = [0.0, DM_stored, 0.0, tau_g, alpha_g]
+            # pptoas.py:474-484 verbatim in effect: get_TOAs keeps one
+            # fit_flags list across subints and archives, and a 2-channel
+            # subint (fit_DM and fit_GM) zeroes GM in the *previous* subint's
+            # list -- phase-only after a 1-channel subint, and an
+            # UnboundLocalError when no subint came before it.
             if len(freqsx) == 1:
                 ff = [1, 0, 0, 0, 0]
+            elif len(freqsx) == 2 and self.fit_DM and self.fit_GM:
+                if self._fit_flags_prev is None:
+                    raise UnboundLocalError(
+                        "local variable 'fit_flags' referenced before assignment")
+                ff = list(self._fit_flags_prev)
+                ff[2] = 0
             else:
                 ff = list(self.fit_flags)
-                if len(freqsx) == 2 and self.fit_DM and self.fit_GM:
-                    ff[2] = 0
+            self._fit_flags_prev = ff
             fit_flags_sub[isub] = ff
             flag_sets.setdefault(tuple(ff), []).append(isub)
+        if bounds is None and method == "TNC":
+            # get_TOAs' default TNC bounds (pptoas.py:458-467)
+            bounds = [(None, None), (None, None), (None, None),
+                      (np.log10((10 * nbin) ** -1), None) if self.log10_tau else (0.0, None),
+                      (-10.0, 10.0)]
         res_all = {}
         fit_duration = 0.0
         for ff, subs in flag_sets.items():
@@ -239,7 +255,8 @@ class GetTOAs:
                 option=0, is_toa=True, chan_mask=mask[subs],
                 weights=data.weights[subs], model_idx=midx[subs], guess=True,
                 guess_Ns=100, guess_wrap=True, guess_nu=None,
-                guess_tau=guess_tau[subs] if fit_scat else None, method=method)
+                guess_tau=guess_tau[subs] if fit_scat else None, method=method,
+                bounds=bounds)
             fit_duration += time.time() - t0
             for j, isub in enumerate(subs):
                 res_all[isub] = (res, j)

@@ -59,12 +59,15 @@ def fit_portraits_batch(data, model, init, P, freqs, nu_fits=None, nu_outs=None,
                         errs=None, fit_flags=(1, 1, 0, 0, 0), log10_tau=False, option=0,
                         is_toa=True, chan_mask=None, weights=None, model_idx=None,
                         guess=False, guess_Ns=100, guess_wrap=True, guess_nu=None,
-                        guess_tau=None, method="trust-ncg", device=None, to_host=True):
-    """Batched fit_portrait_full over subints; returns arrays keyed like its DataBunch."""
-    if method != "trust-ncg":
-        raise NotImplementedError(
-            "method %r: the device solver implements scipy 'trust-ncg' (the "
-            "reference default, pptoaslib.py:932)" % method)
+                        guess_tau=None, method="trust-ncg", bounds=None, device=None,
+                        to_host=True):
+    """Batched fit_portrait_full over subints; returns arrays keyed like its DataBunch.
+
+    method selects the device solver as minimize(method=...) does in the
+    reference (pptoaslib.py:995-1014); bounds are applied by TNC only."""
+    if method not in ("trust-ncg", "TNC", "Newton-CG"):
+        print("Method '%s' is not implemented." % method)
+        sys.exit()
     from .engine import get_engine
     eng = get_engine(device)
     t0 = time.time()
@@ -72,7 +75,8 @@ def fit_portraits_batch(data, model, init, P, freqs, nu_fits=None, nu_outs=None,
                         nu_out=nu_outs, errs=errs, chan_mask=chan_mask, weights=weights,
                         model_idx=model_idx, log10_tau=log10_tau, option=option,
                         is_toa=is_toa, guess=guess, guess_Ns=guess_Ns,
-                        guess_wrap=guess_wrap, guess_nu=guess_nu, guess_tau=guess_tau)
+                        guess_wrap=guess_wrap, guess_nu=guess_nu, guess_tau=guess_tau,
+                        method=method, bounds=bounds if method == "TNC" else None)
     if not to_host:
         return out
     res = {k: v.cpu().numpy() for k, v in out.items() if not k.startswith("_")}
@@ -144,6 +148,6 @@ def fit_portrait_full(data_port, model_port, init_params, P, freqs,
                           list(init_params), P, freqs, nu_fits, nu_outs,
                           None if errs is None else np.asarray(errs, dtype=float),
                           fit_flags, log10_tau, option=option, is_toa=is_toa,
-                          method=method)
+                          method=method, bounds=bounds)
     report_failure(int(res["status"][0]), sub_id)
     return result_bunch(res, 0, fit_flags)

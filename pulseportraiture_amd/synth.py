@@ -137,3 +137,25 @@ def make_workload(nsub, nchan, nbin, seed=20240917, sub0=0, sigma=1.5, tau=0.0,
 
 def workload_data_host(w):
     return synth_portraits_host(w.template, w.phase, w.sigma, w.seed, w.sub0)
+
+
+def _data_chunk(args):
+    nsub, nchan, nbin, seed, sub0, kw = args
+    return np.stack([workload_data_host(make_workload(1, nchan, nbin, seed=seed, sub0=sub0 + i,
+                                                      **kw))[0] for i in range(nsub)])
+
+
+def workload_data_host_parallel(nsub, nchan, nbin, seed=20240917, sub0=0, procs=8, chunk=64,
+                                **kw):
+    """Subints sub0 .. sub0 + nsub - 1, each generated alone (bitwise what
+    workload_data_host(make_workload(1, ..., sub0=i)) gives; a batched irfft
+    can differ in the last bit), in `procs` spawned worker processes (no
+    fork: the caller may own a GPU context)."""
+    import multiprocessing as mp
+    jobs = [(min(chunk, nsub - lo), nchan, nbin, seed, sub0 + lo, kw)
+            for lo in range(0, nsub, chunk)]
+    out = np.empty((nsub, nchan, nbin))
+    with mp.get_context("spawn").Pool(procs) as pool:
+        for j, part in zip(range(0, nsub, chunk), pool.imap(_data_chunk, jobs)):
+            out[j:j + len(part)] = part
+    return out

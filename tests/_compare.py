@@ -1,0 +1,27 @@
+"""Shared parity comparisons for the CPU (oracle) and GPU tests."""
+import numpy as np
+
+DCONST = 0.000241 ** -1  # pplib.py:51
+
+# trust-ncg / TNC return codes the reference treats as converged: it reports
+# a fit as 'failed' only outside this set (pptoaslib.py:1022-1033)
+CONVERGED = {1, 2, 4}
+
+
+def phi_at(phi, DM, GM, nu_DM, nu_GM, to_DM, to_GM, P):
+    """phi reported at (nu_DM, nu_GM) moved to (to_DM, to_GM), wrapped to
+    [-0.5, 0.5) (phase_shifts / phase_transform, pptoaslib.py:181-214)."""
+    out = phi + DCONST * DM / P * (to_DM ** -2 - nu_DM ** -2) + \
+        DCONST ** 2 * GM / P * (to_GM ** -4 - nu_GM ** -4)
+    return (out + 0.5) % 1.0 - 0.5
+
+
+def phase_gap(phi, DM, GM, nu_DM, nu_GM, ref, P):
+    """|phi - phi_ref| / sigma_phi with both phases at the reference's output
+    frequencies.  The zero-covariance frequency is a ratio of Hessian sums
+    that cancel heavily for multi-parameter fits, so two fits that agree to
+    1e-5 sigma can report their TOA at frequencies 1e-8 apart; comparing the
+    phases at one frequency separates the fit from that reporting choice."""
+    p = phi_at(phi, DM, GM, nu_DM, nu_GM, ref["nu_DM"], ref["nu_GM"], P)
+    d = abs(p - ref["phi"])
+    return min(d, 1.0 - d) / ref["phi_err"]

@@ -1,0 +1,173 @@
+"""GPU parity at the BASELINE.json config shapes, against the reference itself.
+
+Fixtures (tests/golden/make_golden_r2.py, the reference run through the
+SURVEY §8(c) shim on Philox-seeded inputs that synth.py regenerates here):
+- configs_r2.*: GetTOAs.get_TOAs on synthetic archives at config 3 (512 ch x
+  1024 bin, phase+DM+tau+alpha, log10 tau) and config 4 (128 ch x 2048 bin,
+  phase+DM+GM);
+- align5.npz: ppalign.align_archives at config 5's shape (256 ch x 2048 bin,
+  guess grid Ns = nbin = 2048: the direct brute-force path), niter 1 and 2;
+- headline_2k.npz: 2000 subints of the bench workload (64 x 2048, phase+DM,
+  get_TOAs guess + trust-ncg) with the reference's own trajectory floor: the
+  same fit restarted from the guess moved by one ulp either way.
+
+Tolerances: north_star |dX| <= 1e-3 sigma_X per fitted parameter and
+identical return codes; .tim flags as a key -> value map.
+"""
+import json
+import os
+import shutil
+
+import numpy as np
+import pytest
+
+from tests.conftest import GOLDEN
+from tests.golden_consts import DM0
+from tests.test_gpu_drivers import mjd_diff_us, parse_tim
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from pulseportraiture_amd.engine import get_engine
+    return get_engine(0)
+
+
+def register_synth_archive(name, nsub, nchan, nbin, seed, tau, gm):
+    """The archive make_golden_r2.synth_archive handed to the reference."""
+    from pulseportraiture_amd import archive, synth
+    from pulseportraiture_amd.mjd import MJD
+    w = synth.make_workload(nsub, nchan, nbin, seed=seed, tau=tau, gm=gm)
+    data = synth.workload_data_host(w)
+    b = dict(subints=data[:, None], freqs=np.tile(w.freqs, (nsub, 1)),
+             weights=np.ones((nsub, nchan)), SNRs=np.ones((nsub, 1, nchan)),
+             Ps=np.full(nsub, w.P), doppler_factors=np.full(nsub, 1.00002),
+             epochs=[MJD(57300.0 + 0.001 * i) + 10.0 for i in range(nsub)], DM=DM0,
+             backend="syn_be", frontend="syn_rx", backend_delay=2.0e-6, telescope="GBT",
+             telescope_code="1", bw=800.0, nu0=1500.0, subtimes=[30.0] * nsub, prof_SNR=100.0)
+    archive.register_archive(name, b)  # noise_stds estimated on the device
+    return w
+
+
+def compare_tim(lines, ref):
+    assert len(lines) == len(ref)
+    for ours, theirs in zip(lines, ref):
+        h1, f1 = parse_tim(ours)
+        h2, f2 = parse_tim(theirs)
+        assert h1["archive"] == h2["archive"] and h1["site"] == h2["site"]
+        assert abs(h1["freq"] - h2["freq"]) < 1e-5 * max(1.0, h2["freq"] * 1e-3)
+        assert abs(mjd_diff_us(h1["mjd"], h2["mjd"])) <= 1e-3 * h2["err"] + 2e-4
+        assert abs(h1["err"] - h2["err"]) <= 2e-3
+        assert set(f1) == set(f2)
+        for k, v in f2.items():
+            try:
+                a, b = float(f1[k]), float(v)
+            except ValueError:
+                assert f1[k] == v, k
+                continue
+            if k == "pp_dm":
+                tol = max(1e-3 * float(f2.get("pp_dme", 0)), 1.1e-7)
+            elif k == "pp_dme":
+                tol = 1e-4 * b + 1.1e-7
+            elif k in ("gm", "gm_err"):
+                tol = 1e-3 * float(f2.get("gm_err", 1)) + 1.1e-3
+            elif k in ("scat_time", "log10_scat_time", "scat_ind"):
+                tol = 1.1e-3 + 1e-5 * abs(b)
+            else:
+                tol = 1.1e-3 + 1e-6 * abs(b) if "." in v else 0.5
+            assert abs(a - b) <= tol, (k, f1[k], v)
+
+
+@pytest.mark.parametrize("name", ["cfg3", "cfg4"])
+def test_get_toas_config_shapes(gpu, name, tmp_path):
+    from pulseportraiture_amd import pplib, pptoas, synth
+    meta = json.load(open(os.path.join(GOLDEN, "configs_r2.json")))[name]
+    z = np.load(os.path.join(GOLDEN, "configs_r2.npz"))
+    register_synth_archive(name + ".fits", meta["nsub"], meta["nchan"], meta["nbin"],
+                           meta["seed"], meta["tau"], meta["gm"])
+    shutil.copy(synth.EXAMPLE_GMODEL, os.path.join(tmp_path, "example.gmodel"))
+    cwd = os.getcwd()
+    os.chdir(tmp_path)
+    try:
+        gt = pptoas.GetTOAs([name + ".fits"], "example.gmodel", quiet=True)
+        gt.get_TOAs(quiet=True, **meta["kwargs"])
+        lines = [pplib.toa_line(t) for t in gt.TOA_list]
+    finally:
+        os.chdir(cwd)
+    p = name + "_"
+    assert np.array_equal(gt.rcs[0], z[p + "rcs"]), (gt.rcs[0], z[p + "rcs"])
+    for attr in ["phi", "DM", "GM", "tau", "alpha"]:
+        err = z[p + attr + "_errs"]
+        got, ref = np.asarray(getattr(gt, attr + "s")[0]), z[p + attr + "s"]
+        fitted = err > 0
+        assert np.all(np.abs(got - ref)[fitted] <= 1e-3 * err[fitted]), (attr, got, ref, err)
+        np.testing.assert_allclose(np.asarray(getattr(gt, attr + "_errs")[0])[fitted],
+                                   err[fitted], rtol=1e-5, err_msg=attr)
+    np.testing.assert_allclose(gt.snrs[0], z[p + "snrs"], rtol=1e-6)
+    np.testing.assert_allclose(gt.red_chi2s[0], z[p + "red_chi2s"], rtol=1e-8)
+    np.testing.assert_allclose(np.array(gt.nu_refs[0], float), z[p + "nu_refs"], rtol=1e-6)
+    compare_tim(lines, meta["tim"])
+    print("%s nfev device %s reference %s" % (name, list(gt.nfevals[0]),
+                                              list(z[p + "nfevals"].astype(int))))
+
+
+def test_align_archives_config5_shape(gpu):
+    from oracle import ppfit_oracle as O
+    from pulseportraiture_amd import archive, ppalign, synth
+    z = np.load(os.path.join(GOLDEN, "align5.npz"))
+    n, nchan, nbin = int(z["cfg_narch"]), int(z["cfg_nchan"]), int(z["cfg_nbin"])
+    seed = int(z["cfg_seed"])
+    names = ["a5_%d.fits" % i for i in range(n)]
+    for i, nm in enumerate(names):
+        register_synth_archive(nm, 1, nchan, nbin, seed + i, 0.0, 0.0)
+    w = synth.make_workload(1, nchan, nbin, seed=seed)
+    guess = O.rotate_data(w.model, float(z["cfg_guess_rot"]))
+    archive.register_archive("guess5.fits", dict(subints=guess[None, None], freqs=w.freqs,
+                                                 Ps=[w.P], epochs=[(57300, 0, 0.0)], DM=DM0))
+    k = np.arange(nbin)
+    for niter in (1, 2):
+        port = ppalign.align_archives(names, "guess5.fits", fit_dm=True, niter=niter,
+                                      quiet=True)[0]
+        np.testing.assert_allclose(port.sum(axis=1), z["niter%d_chan_sum" % niter],
+                                   rtol=1e-6, atol=1e-9 * np.abs(port).sum())
+        np.testing.assert_allclose((port ** 2).sum(axis=1), z["niter%d_chan_sum2" % niter],
+                                   rtol=1e-6)
+        np.testing.assert_allclose((port * k).sum(axis=1), z["niter%d_chan_moment" % niter],
+                                   rtol=1e-6, atol=1e-6 * np.abs(port * k).sum(axis=1).max())
+        if niter == 2:
+            ref = z["aligned_niter2_f32"].astype(np.float64)
+            np.testing.assert_allclose(port, ref, atol=2e-6 * np.abs(ref).max())
+
+
+def test_headline_2000_subints_vs_reference(gpu):
+    """Config 2 (64 x 2048, phase+DM, guess + trust-ncg) over 2000 subints."""
+    from pulseportraiture_amd import synth
+    import os as _os
+    z = np.load(os.path.join(GOLDEN, "headline_2k.npz"))
+    nsub, seed = int(z["nsub"]), int(z["seed"])
+    procs = min(16, _os.cpu_count() or 1)
+    data = synth.workload_data_host_parallel(nsub, 64, 2048, seed=seed, procs=procs)
+    w = synth.make_workload(1, 64, 2048, seed=seed)
+    nu = z["nu_fit"]
+    out = gpu.fit_batch(data, w.model, w.freqs, w.P, [0.0, DM0, 0, 0, 0], [1, 1, 0, 0, 0],
+                        nu_fit=np.stack([nu] * 3, 1), guess=True, guess_Ns=100)
+    r = {k: v.cpu().numpy() for k, v in out.items() if not k.startswith("_")}
+    np.testing.assert_allclose(r["init_used"][:, 0], z["phi_guess"], rtol=0, atol=1e-6)
+    st = r["status"]
+    assert np.array_equal(st, z["status"].astype(int)), np.where(st != z["status"])
+    dphi = np.abs(r["params"][:, 0] - z["phi"]) / z["phi_err"]
+    ddm = np.abs(r["params"][:, 1] - z["DM"]) / z["DM_err"]
+    floor = np.maximum(np.abs(z["up_phi"] - z["phi"]), np.abs(z["dn_phi"] - z["phi"])) / z["phi_err"]
+    print("headline 2k |dphi|/sigma p50 %.3g p99 %.3g max %.3g (reference 1-ulp floor: p99 "
+          "%.3g max %.3g); |dDM|/sigma max %.3g; nu_DM max rel %.3g" % (
+              np.median(dphi), np.percentile(dphi, 99), dphi.max(),
+              np.percentile(floor, 99), floor.max(), ddm.max(),
+              np.max(np.abs(r["nu_out"][:, 0] / z["nu_DM"] - 1))))
+    assert dphi.max() <= 1e-3 and ddm.max() <= 1e-3
+    np.testing.assert_allclose(r["param_errs"][:, 0], z["phi_err"], rtol=1e-6)
+    np.testing.assert_allclose(r["red_chi2"], z["red_chi2"], rtol=1e-9)
+    np.testing.assert_allclose(r["snr"], z["snr"], rtol=1e-8)
