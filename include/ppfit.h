@@ -105,6 +105,9 @@ int ppf_phase_profile(ppf_ctx* ctx, int32_t enable, uint64_t* out);
 #define PPF_METHOD_TRUST_NCG 0   /* scipy trust-ncg, gtol = -1 (the default)  */
 #define PPF_METHOD_TNC 1         /* scipy TNC with bounds, xtol 1e-10, minfev */
 #define PPF_METHOD_NEWTON_CG 2   /* scipy Newton-CG, xtol = -1, maxiter 2000   */
+#define PPF_METHOD_TNC_LEGACY 3  /* pplib.fit_portrait: TNC over (phase, DM) only,
+                                    xtol 1e-10 (pplib.py:2144-2148); fit_flags
+                                    must be [1,1,0,0,0]                        */
 
 /* Phase-family fits (tau = 0 and not fitted) evaluate the objective from
  * per-channel Taylor moments of the cross-spectrum (no nchan x nharm

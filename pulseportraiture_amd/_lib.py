@@ -14,8 +14,9 @@ PPF_OK = 0
 PPF_METHOD_TRUST_NCG = 0
 PPF_METHOD_TNC = 1
 PPF_METHOD_NEWTON_CG = 2
+PPF_METHOD_TNC_LEGACY = 3
 METHODS = {"trust-ncg": PPF_METHOD_TRUST_NCG, "TNC": PPF_METHOD_TNC,
-           "Newton-CG": PPF_METHOD_NEWTON_CG}
+           "Newton-CG": PPF_METHOD_NEWTON_CG, "TNC-legacy": PPF_METHOD_TNC_LEGACY}
 KERNEL_IDS = {"model_fft": 0, "data_xspec": 1, "solve": 2, "phase_shift": 3,
               "rotate": 4, "rot_accum": 5, "synth": 6, "irfft": 7, "noise": 8,
               "guess": 9, "post": 10, "fit_taylor": 11, "moments": 12}

@@ -274,8 +274,13 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   if (d->nchan <= 0 || d->nchan > PPF_MAX_NCHAN)
     return fail(ctx, PPF_ERR_UNSUPPORTED, "nchan=%d outside [1, %d]", d->nchan, PPF_MAX_NCHAN);
   if (d->nmodel <= 0) return fail(ctx, PPF_ERR_INVALID, "nmodel must be >= 1");
-  if (d->method != PPF_METHOD_TRUST_NCG)
+  const bool tnc = d->method == PPF_METHOD_TNC || d->method == PPF_METHOD_TNC_LEGACY;
+  if (d->method != PPF_METHOD_TRUST_NCG && !tnc)
     return fail(ctx, PPF_ERR_UNSUPPORTED, "Method %d is not implemented.", d->method);
+  if (d->method == PPF_METHOD_TNC_LEGACY &&
+      !(d->fit_flags[0] && d->fit_flags[1] && !d->fit_flags[2] && !d->fit_flags[3] &&
+        !d->fit_flags[4]))
+    return fail(ctx, PPF_ERR_INVALID, "legacy TNC fits phase and DM only (fit_flags [1,1,0,0,0])");
   if (d->solver_flags & ~(PPF_SOLVE_EXACT | PPF_SOLVE_EVAL | PPF_GUESS_DIRECT))
     return fail(ctx, PPF_ERR_INVALID, "unknown solver_flags bits 0x%x", d->solver_flags);
   if (!d->data || !d->model || !d->freqs || !d->P || !d->init || !d->nu_fit || !d->nu_out)
@@ -301,7 +306,7 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   // subints are fitted from Taylor moments of it (k_fit_taylor); scattering
   // fits, and every fit under PPF_SOLVE_EXACT, sweep it directly.
   const bool exact = (d->solver_flags & PPF_SOLVE_EXACT) != 0;
-  const bool taylor = !exact;
+  const bool taylor = !exact && d->method == PPF_METHOD_TRUST_NCG;
   // mean template spectrum for the unmasked guess
   double2* Mmean = nullptr;
   if (d->guess) {
@@ -441,6 +446,11 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
     // each subint runs in exactly one of the exact phase-only / scattering /
     // fused Taylor variants (the others exit at once)
     if (int r = timed(ctx, PPF_K_SOLVE, [&] {
+          if (tnc) {
+            hipLaunchKernelGGL(k_tnc<false>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
+            hipLaunchKernelGGL(k_tnc<true>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
+            return;
+          }
           if (exact)
             hipLaunchKernelGGL(k_solve<false>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
           hipLaunchKernelGGL(k_solve<true>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);

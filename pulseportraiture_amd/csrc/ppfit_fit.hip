@@ -864,6 +864,7 @@ __global__ __launch_bounds__(kBlock) void k_solve(FitArgs a) {
   __shared__ double refs[3];
   const int c = blockIdx.x, s = a.sub0 + c, tid = threadIdx.x;
   const int lane = tid & 63;
+  if (a.method != PPF_METHOD_TRUST_NCG) return;  // k_tnc owns TNC fits
   if ((a.st[c].scat != 0) != SCAT) return;  // the other variant owns this subint
   const Meta m = load_meta(a, c, s, dyn, &sh.nok);
   SolveState& st = a.st[c];

@@ -187,10 +187,78 @@ __device__ __forceinline__ double block_eval_phase(const double2* rm, int NH, do
   return t;
 }
 
+// One brute-force pass over the grid: FOLD evaluates the folded L-point DFT
+// (gs.fb / gs.fw ready), else direct sums.  Leaves the argmin in
+// gs.bestv[0] / gs.besti[0] and gs.x0; returns this thread's grid value for
+// the single chunk of a FOLD pass (NaN otherwise).
+template <bool FOLD>
+__device__ __forceinline__ double brute_pass(const double2* rm, int NH, double ie2, int Ns,
+                                             double lo, double hi, GuessShared& gs) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  constexpr int GP = kBlock / 2;
+  const double step = (hi - lo) / (double)(Ns - 1);
+  const int half = tid / GP, gl = tid % GP;
+  const int kmid = (NH + 1) / 2;
+  const int L = Ns - 1;
+  double bv = NAN, myf = NAN;
+  int bi = 0x7fffffff;
+  for (int g0 = 0; g0 < Ns; g0 += GP) {
+    const int g = g0 + gl;
+    double part = 0.0;
+    if (g < Ns) {
+      if constexpr (FOLD) {
+        const int jm = (L + 1) / 2;
+        const int j0 = half ? jm : 0, j1 = half ? L : jm;
+        int mi = (j0 * g) % L;
+        for (int j = j0; j < j1; ++j) {
+          const double2 b = gs.fb[j], wv = gs.fw[mi];
+          part = fma(b.x, wv.x, part);
+          part = fma(-b.y, wv.y, part);
+          mi += g;
+          if (mi >= L) mi -= L;
+        }
+      } else {
+        const double ph = (g == Ns - 1) ? hi : __dadd_rn(__dmul_rn((double)g, step), lo);
+        part = half ? row_eval_phase(rm, kmid, NH, ph) : row_eval_phase(rm, 0, kmid, ph);
+      }
+    }
+    gs.bf[tid] = part;
+    __syncthreads();
+    if (tid < GP && g < Ns) {
+      const double f = -(gs.bf[tid] + gs.bf[GP + tid]) * ie2;
+      myf = f;
+      if (argmin_better(f, g, bv, bi)) { bv = f; bi = g; }
+    }
+    __syncthreads();
+  }
+  // argmin over the owning threads (ascending g within a thread)
+  if (tid < GP) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const double ov = __shfl_xor(bv, o);
+      const int oi = __shfl_xor(bi, o);
+      if (argmin_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+    }
+    if (lane == 0) { gs.bestv[w] = bv; gs.besti[w] = bi; }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double v = gs.bestv[0];
+    int i = gs.besti[0];
+    for (int q = 1; q < GP / 64; ++q)
+      if (argmin_better(gs.bestv[q], gs.besti[q], v, i)) { v = gs.bestv[q]; i = gs.besti[q]; }
+    gs.x0 = (i == Ns - 1) ? hi : __dadd_rn(__dmul_rn((double)i, step), lo);
+    gs.bestv[0] = v;
+    gs.besti[0] = i;
+  }
+  __syncthreads();
+  return myf;
+}
+
 __device__ inline void guess_search(const double2* rm, int NH, double ie2, int Ns, double lo,
                                     double hi, GuessShared& gs, bool allow_fold = true,
                                     unsigned long long* clk = nullptr) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x;
   // diagnostic clocks (ppf_phase_profile): [0] brute force, [1] Nelder-Mead, [2] NM calls
   const unsigned long long c0 = clk ? wall_clock64() : 0ull;
   // ---- brute force over the inclusive grid (np.mgrid[lo:hi:Ns*1j]) ----
@@ -198,10 +266,6 @@ __device__ inline void guess_search(const double2* rm, int NH, double ie2, int N
   // contract them into FMAs and move the points off numpy's values.
   // Threads own grid points (kBlock / 2 per chunk) and walk half of the
   // harmonics each; the halves meet in LDS.
-  constexpr int GP = kBlock / 2;
-  const double step = (hi - lo) / (double)(Ns - 1);
-  const int half = tid / GP, gl = tid % GP;
-  const int kmid = (NH + 1) / 2;
   // On the get_TOAs grid (lo, hi) = (-0.5, 0.5) every grid phase is
   // -1/2 + g / L, L = Ns - 1, so f(phi_g) = Re sum_j b_j w^{j g} with the
   // spectrum folded mod L: an L-point DFT instead of Ns x NH phasor terms.
@@ -212,85 +276,31 @@ __device__ inline void guess_search(const double2* rm, int NH, double ie2, int N
   // The folded values round differently from the direct sums, so when any
   // other grid point comes within 1e-12 (relative) of the minimum the grid
   // is re-taken by direct sums and np.argmin decides on those.
+  constexpr int GP = kBlock / 2;
   const int L = Ns - 1;
-  bool fold = allow_fold && lo == -0.5 && hi == 0.5 && L >= 2 && L <= GP && NH > 2 * L;
-  for (int pass = 0; pass < 2; ++pass) {
-    double bv = NAN;
-    int bi = 0x7fffffff;
-    double myf = NAN;  // fold pass: this thread's grid value (one chunk)
-    if (fold) {
-      if (tid < L) {
-        double2 b = cmk(0.0, 0.0);
-        for (int k = tid; k < NH; k += L) {
-          const double2 r = rm[k];
-          b = (k & 1) ? csub(b, r) : cadd(b, r);
-        }
-        gs.fb[tid] = b;
-        double sn, cs;
-        sincospi(2.0 * (double)tid / (double)L, &sn, &cs);
-        gs.fw[tid] = cmk(cs, sn);
+  const bool fold = allow_fold && lo == -0.5 && hi == 0.5 && L >= 2 && L <= GP && NH > 2 * L;
+  if (fold) {
+    if (tid < L) {
+      double2 b = cmk(0.0, 0.0);
+      for (int k = tid; k < NH; k += L) {
+        const double2 r = rm[k];
+        b = (k & 1) ? csub(b, r) : cadd(b, r);
       }
-      __syncthreads();
-    }
-    for (int g0 = 0; g0 < Ns; g0 += GP) {
-      const int g = g0 + gl;
-      double part = 0.0;
-      if (g < Ns) {
-        if (fold) {
-          const int jm = (L + 1) / 2;
-          const int j0 = half ? jm : 0, j1 = half ? L : jm;
-          int mi = (j0 * g) % L;
-          for (int j = j0; j < j1; ++j) {
-            const double2 b = gs.fb[j], wv = gs.fw[mi];
-            part = fma(b.x, wv.x, part);
-            part = fma(-b.y, wv.y, part);
-            mi += g;
-            if (mi >= L) mi -= L;
-          }
-        } else {
-          const double ph = (g == Ns - 1) ? hi : __dadd_rn(__dmul_rn((double)g, step), lo);
-          part = half ? row_eval_phase(rm, kmid, NH, ph) : row_eval_phase(rm, 0, kmid, ph);
-        }
-      }
-      gs.bf[tid] = part;
-      __syncthreads();
-      if (tid < GP && g < Ns) {
-        const double f = -(gs.bf[tid] + gs.bf[GP + tid]) * ie2;
-        myf = f;
-        if (argmin_better(f, g, bv, bi)) { bv = f; bi = g; }
-      }
-      __syncthreads();
-    }
-    // argmin over the owning threads (ascending g within a thread)
-    if (tid < GP) {
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const double ov = __shfl_xor(bv, o);
-        const int oi = __shfl_xor(bi, o);
-        if (argmin_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
-      }
-      if (lane == 0) { gs.bestv[w] = bv; gs.besti[w] = bi; }
+      gs.fb[tid] = b;
+      double sn, cs;
+      sincospi(2.0 * (double)tid / (double)L, &sn, &cs);
+      gs.fw[tid] = cmk(cs, sn);
     }
     __syncthreads();
-    if (tid == 0) {
-      double v = gs.bestv[0];
-      int i = gs.besti[0];
-      for (int q = 1; q < GP / 64; ++q)
-        if (argmin_better(gs.bestv[q], gs.besti[q], v, i)) { v = gs.bestv[q]; i = gs.besti[q]; }
-      gs.x0 = (i == Ns - 1) ? hi : __dadd_rn(__dmul_rn((double)i, step), lo);
-      gs.bestv[0] = v;
-      gs.besti[0] = i;
-    }
-    __syncthreads();
-    if (!fold) break;
+    const double myf = brute_pass<true>(rm, NH, ie2, Ns, lo, hi, gs);
     // near tie on the folded grid (the end points -0.5 / 0.5 are one point)
     const double v = gs.bestv[0];
     const int i = gs.besti[0];
     const bool endpair = (i == 0 && tid == Ns - 1) || (i == Ns - 1 && tid == 0);
-    const bool near = tid < GP && tid < Ns && tid != i && !endpair &&
-                      !(fabs(myf - v) > 1e-12 * fabs(v));
-    if (!__syncthreads_or(near)) break;
-    fold = false;
+    const bool near = tid < Ns && tid != i && !endpair && !(fabs(myf - v) > 1e-12 * fabs(v));
+    if (__syncthreads_or(near)) brute_pass<false>(rm, NH, ie2, Ns, lo, hi, gs);
+  } else {
+    brute_pass<false>(rm, NH, ie2, Ns, lo, hi, gs);
   }
   const unsigned long long c1 = clk ? wall_clock64() : 0ull;
   // ---- Nelder-Mead polish: every thread runs the (uniform, scalar) simplex
@@ -387,6 +397,7 @@ template <int U>
 __global__ void k_moments(FitArgs a);
 __global__ void k_selftest(int* fails);
 template <bool SCAT> __global__ void k_solve(FitArgs a);
+template <bool SCAT> __global__ void k_tnc(FitArgs a);
 template <bool SCAT> __global__ void k_post(FitArgs a);
 
 }  // namespace ppf

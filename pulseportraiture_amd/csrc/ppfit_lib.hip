@@ -2,4 +2,5 @@
 #include "ppfit_spectra.hip"
 #include "ppfit_fit.hip"
 #include "ppfit_taylor.hip"
+#include "ppfit_tnc.hip"
 #include "ppfit_capi.hip"

@@ -344,22 +344,25 @@ def fit_phase_shift(data, model, noise=None, bounds=[-0.5, 0.5], Ns=100):
 
 def fit_portrait(data, model, init_params, P, freqs, nu_fit=None, nu_out=None, errs=None,
                  bounds=[(None, None), (None, None)], id=None, quiet=True):
-    """Legacy phase + DM fit (pplib.py:2102-2204) on the GPU objective.
+    """Legacy phase + DM fit (pplib.py:2102-2204) on the GPU.
 
-    The reference minimises with scipy TNC; this drop-in runs the batched
-    trust-region Newton solver on the same objective (same optimum; see
-    DESIGN.md) and reports the legacy outputs: phase/DM errors from the
-    2x2 curvature matrix without amplitude covariance (pplib.py:2184-2190)
-    and scale_errs = (p_n / errs^2)^-1/2 (pplib.py:2197).
+    As the reference, scipy TNC (jac, bounds, xtol 1e-10; pplib.py:2144-2148)
+    over (phase, DM) -- the device TNC (ppfit_tnc.hip) in its 2-parameter
+    form -- then the legacy outputs: phase/DM errors from the 2x2 curvature
+    matrix without amplitude covariance (pplib.py:2184-2190) and scale_errs
+    = (p_n / errs^2)^-1/2 (pplib.py:2197).  return_code and nfeval are TNC's
+    (RCSTRINGS, pplib.py:111-119).
     """
     from . import pptoaslib
     freqs = np.asarray(freqs, dtype=float)
     if nu_fit is None:
         nu_fit = freqs.mean()
+    b = list(bounds) if bounds is not None else [(None, None)] * 2
     res = pptoaslib._fit_batch_host(
         np.asarray(data, float)[None], np.asarray(model, float)[None], [init_params[0],
         init_params[1], 0.0, 0.0, 0.0], P, freqs, [nu_fit, nu_fit, nu_fit],
-        [nu_out, nu_out, nu_out], errs, [1, 1, 0, 0, 0], log10_tau=False, legacy=True)
+        [nu_out, nu_out, nu_out], errs, [1, 1, 0, 0, 0], log10_tau=False, legacy=True,
+        method="TNC-legacy", bounds=b + [(None, None)] * 3)
     r = {k: v[0] for k, v in res.items() if k != "legacy"}
     leg = {k: v[0] for k, v in res["legacy"].items()}
     return DataBunch(phase=r["params"][0], phase_err=leg["phase_err"], DM=r["params"][1],

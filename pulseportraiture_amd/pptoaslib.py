@@ -65,7 +65,7 @@ def fit_portraits_batch(data, model, init, P, freqs, nu_fits=None, nu_outs=None,
 
     method selects the device solver as minimize(method=...) does in the
     reference (pptoaslib.py:995-1014); bounds are applied by TNC only."""
-    if method not in ("trust-ncg", "TNC", "Newton-CG"):
+    if method not in ("trust-ncg", "TNC", "Newton-CG", "TNC-legacy"):
         print("Method '%s' is not implemented." % method)
         sys.exit()
     from .engine import get_engine
@@ -76,7 +76,7 @@ def fit_portraits_batch(data, model, init, P, freqs, nu_fits=None, nu_outs=None,
                         model_idx=model_idx, log10_tau=log10_tau, option=option,
                         is_toa=is_toa, guess=guess, guess_Ns=guess_Ns,
                         guess_wrap=guess_wrap, guess_nu=guess_nu, guess_tau=guess_tau,
-                        method=method, bounds=bounds if method == "TNC" else None)
+                        method=method, bounds=bounds if method.startswith("TNC") else None)
     if not to_host:
         return out
     res = {k: v.cpu().numpy() for k, v in out.items() if not k.startswith("_")}
@@ -139,7 +139,7 @@ def fit_portrait_full(data_port, model_port, init_params, P, freqs,
                       log10_tau=True, option=0, sub_id=None, method="trust-ncg",
                       is_toa=True, quiet=True):
     """Fit phase, DM, GM, tau, alpha between data and model portraits (pptoaslib.py:928)."""
-    if method not in ("trust-ncg", "TNC", "Newton-CG"):
+    if method not in ("trust-ncg", "TNC", "Newton-CG", "TNC-legacy"):
         print("Method '%s' is not implemented." % method)
         sys.exit()
     data_port = np.asarray(data_port, dtype=float)
