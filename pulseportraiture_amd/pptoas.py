@@ -21,6 +21,24 @@ max_nfile = 999
 rm_baseline = bool(F0_fact)  # pptoas.py:25-29
 
 
+def _dist_info():
+    """(rank, world) of an initialised torch.distributed group, else (0, 1)."""
+    try:
+        import torch.distributed as dist
+    except ImportError:
+        return 0, 1
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def _shard_range(n, rank, world):
+    """Contiguous [lo, hi) of n units for rank; sizes differ by at most one."""
+    base, extra = divmod(n, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
 class TOA:
     """TOA record, pptoas.py:31-73."""
 
@@ -136,6 +154,8 @@ class GetTOAs:
         self._fit_flags_prev = None  # the reference's loop-carried fit_flags
         start = time.time()
         datafiles = self.datafiles if datafile is None else [datafile]
+        # 1. load and prepare every archive (all ranks: host bookkeeping only)
+        jobs = []
         for iarch, datafile in enumerate(datafiles):
             try:
                 data = _arch.load_data(datafile, dedisperse=False, dededisperse=False,
@@ -153,18 +173,43 @@ class GetTOAs:
                     print("Cannot load_data(%s).  Skipping it." % datafile)
                 continue
             name = datafile if isinstance(datafile, str) else data.filename
-            self._archive_toas(name, data, nu_refs, nu_fits, fit_scat, log10_tau,
-                               scat_guess, print_phase, print_flux, print_parangle,
-                               addtnl_toa_flags, method, bounds, quiet, already_warned)
+            job = self._prepare(name, data, nu_refs, nu_fits, fit_scat, method, bounds, quiet)
+            if job is not None:
+                jobs.append(job)
+        # 2. fit: the (archive, subint) units in get_TOAs order are split into
+        #    contiguous shards, one per rank (torch.distributed, one process per
+        #    GPU); no collective on the fit path
+        rank, world = _dist_info()
+        units = [(ij, isub) for ij, job in enumerate(jobs) for isub in job.ok_isubs]
+        lo, hi = _shard_range(len(units), rank, world)
+        results, durations = self._fit_units(jobs, units[lo:hi], fit_scat, method)
+        # 3. gather every rank's per-subint results (small host dicts), then
+        #    every rank assembles the same TOAs in the reference's order
+        if world > 1:
+            import torch.distributed as dist
+            parts = [None] * world
+            dist.all_gather_object(parts, (results, durations))
+            results, durations = {}, {}
+            for res_r, dur_r in parts:
+                results.update(res_r)
+                for ij, t in dur_r.items():
+                    durations[ij] = durations.get(ij, 0.0) + t
+        for ij, job in enumerate(jobs):
+            res_all = {isub: results[(ij, isub)] for isub in job.ok_isubs}
+            self._assemble(job.name, job.data, job.obs, job.DM0, job.MJDs, job.ok_isubs,
+                           job.fit_flags_sub, res_all, job.nu_fits_a, job.nu_refs_a,
+                           job.models, job.midx, print_phase, print_flux, print_parangle,
+                           addtnl_toa_flags, durations.get(ij, 0.0), quiet)
         tot = time.time() - start
         if not quiet and len(self.ok_isubs):
             n = np.array([len(x) for x in self.ok_isubs]).sum()
             print("--------------------------")
             print("Total time: %.2f sec, ~%.4f sec/TOA" % (tot, tot / n))
 
-    def _archive_toas(self, datafile, data, nu_ref_tuple, nu_fit_tuple, fit_scat, log10_tau,
-                      scat_guess, print_phase, print_flux, print_parangle, addtnl_toa_flags,
-                      method, bounds, quiet, already_warned):
+    def _prepare(self, datafile, data, nu_ref_tuple, nu_fit_tuple, fit_scat, method, bounds,
+                 quiet):
+        """Per-archive set-up of pptoas.py:246-484: templates, reference
+        frequencies, initial parameters and the per-subint fit flags."""
         nsub, nchan, nbin = data.nsub, data.nchan, data.nbin
         obs = DataBunch(telescope=data.telescope, backend=data.backend, frontend=data.frontend)
         DM_stored = data.DM
@@ -175,12 +220,8 @@ class GetTOAs:
         if mm is None:
             if not quiet:
                 print("Model nbin/nchan mismatch for %s; skipping it." % datafile)
-            return
+            return None
         models, midx, _ = mm
-        subints = np.asarray(data.subints)[:, 0]
-        if data.get("noise_stds") is None:
-            from .engine import get_engine
-            data.noise_stds = get_engine().noise_rows(subints).cpu().numpy()[:, None]
         mask = np.zeros((nsub, nchan), dtype=np.uint8)
         for isub in ok_isubs:
             mask[isub, data.ok_ichans[isub]] = 1
@@ -189,7 +230,6 @@ class GetTOAs:
         nu_refs_a = np.full((nsub, 3), np.nan)
         init = np.zeros((nsub, 5))
         guess_tau = np.zeros(nsub)
-        flag_sets = {}
         fit_flags_sub = {}
         for isub in ok_isubs:
             ok = data.ok_ichans[isub]
@@ -237,32 +277,50 @@ class GetTOAs:
                 ff = list(self.fit_flags)
             self._fit_flags_prev = ff
             fit_flags_sub[isub] = ff
-            flag_sets.setdefault(tuple(ff), []).append(isub)
         if bounds is None and method == "TNC":
             # get_TOAs' default TNC bounds (pptoas.py:458-467)
             bounds = [(None, None), (None, None), (None, None),
                       (np.log10((10 * nbin) ** -1), None) if self.log10_tau else (0.0, None),
                       (-10.0, 10.0)]
-        res_all = {}
-        fit_duration = 0.0
-        for ff, subs in flag_sets.items():
-            subs = np.array(subs)
-            t0 = time.time()
-            res = fit_portraits_batch(
-                subints[subs], models, init[subs], data.Ps[subs], data.freqs[subs],
-                nu_fits=nu_fits_a[subs], nu_outs=nu_refs_a[subs],
-                errs=data.noise_stds[subs, 0], fit_flags=list(ff), log10_tau=self.log10_tau,
-                option=0, is_toa=True, chan_mask=mask[subs],
-                weights=data.weights[subs], model_idx=midx[subs], guess=True,
-                guess_Ns=100, guess_wrap=True, guess_nu=None,
-                guess_tau=guess_tau[subs] if fit_scat else None, method=method,
-                bounds=bounds)
-            fit_duration += time.time() - t0
-            for j, isub in enumerate(subs):
-                res_all[isub] = (res, j)
-        self._assemble(datafile, data, obs, DM0, MJDs, ok_isubs, fit_flags_sub, res_all,
-                       nu_fits_a, nu_refs_a, models, midx, print_phase, print_flux,
-                       print_parangle, addtnl_toa_flags, fit_duration, quiet)
+        return DataBunch(name=datafile, data=data, obs=obs, DM0=DM0, MJDs=MJDs,
+                         ok_isubs=ok_isubs, models=models, midx=midx, mask=mask,
+                         nu_fits_a=nu_fits_a, nu_refs_a=nu_refs_a, init=init,
+                         guess_tau=guess_tau, fit_flags_sub=fit_flags_sub, bounds=bounds)
+
+    def _fit_units(self, jobs, units, fit_scat, method):
+        """Fit this rank's (archive, subint) units: one batched device call per
+        archive and flag set.  Returns {(archive, subint): one-row result dict}
+        and the fit wall time per archive."""
+        results, durations = {}, {}
+        by_arch = {}
+        for ij, isub in units:
+            by_arch.setdefault(ij, []).append(isub)
+        for ij, subs_all in by_arch.items():
+            job = jobs[ij]
+            data = job.data
+            subints = np.asarray(data.subints)[:, 0]
+            errs = None if data.get("noise_stds") is None else data.noise_stds[:, 0]
+            flag_sets = {}
+            for isub in subs_all:
+                flag_sets.setdefault(tuple(job.fit_flags_sub[isub]), []).append(isub)
+            for ff, subs in flag_sets.items():
+                subs = np.array(subs)
+                t0 = time.time()
+                # errs None: the device estimates get_noise_PS per channel,
+                # as load_data's noise_stds (pplib.py:2744-2748)
+                res = fit_portraits_batch(
+                    subints[subs], job.models, job.init[subs], data.Ps[subs], data.freqs[subs],
+                    nu_fits=job.nu_fits_a[subs], nu_outs=job.nu_refs_a[subs],
+                    errs=None if errs is None else errs[subs], fit_flags=list(ff),
+                    log10_tau=self.log10_tau, option=0, is_toa=True,
+                    chan_mask=job.mask[subs], weights=data.weights[subs],
+                    model_idx=job.midx[subs], guess=True, guess_Ns=100, guess_wrap=True,
+                    guess_nu=None, guess_tau=job.guess_tau[subs] if fit_scat else None,
+                    method=method, bounds=job.bounds)
+                durations[ij] = durations.get(ij, 0.0) + time.time() - t0
+                for j, isub in enumerate(subs):
+                    results[(ij, int(isub))] = {k: np.asarray(v)[j:j + 1] for k, v in res.items()}
+        return results, durations
 
     def _assemble(self, datafile, data, obs, DM0, MJDs, ok_isubs, fit_flags_sub, res_all,
                   nu_fits_a, nu_refs_a, models, midx, print_phase, print_flux,
@@ -284,7 +342,7 @@ class GetTOAs:
         nu_fits = list(nu_fits_a)
         nu_refs = [list(r) for r in nu_refs_a]
         for isub in ok_isubs:
-            res, j = res_all[isub]
+            res, j = res_all[int(isub)], 0
             ff = fit_flags_sub[isub]
             ok = data.ok_ichans[isub]
             freqsx = data.freqs[isub, ok]

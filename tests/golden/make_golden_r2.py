@@ -24,6 +24,8 @@ Fixtures:
                      and the reference's own floor -- the same fit restarted
                      from the guess moved by one ulp either way
   timing_r2.json     oracle vs reference wall time per TOA (BASELINE.md:47)
+  tnc_floor.npz      the reference's TNC restarted 1-10 ulps away: how far its
+                     own end point moves (legacy fit and the TNC fit cases)
 
 Usage:  python tests/golden/make_golden_r2.py [fit|configs|align|headline|timing ...]
 """
@@ -387,8 +389,61 @@ def gen_timing(pplib, pptoaslib, n=24):
         json.dump(res, f, indent=1, sort_keys=True)
 
 
+# --------------------------------------------------------------------------
+# TNC's own floor: the reference restarted a few ulps away (legacy fit and
+# the fit_full_r2 TNC cases).  TNC stops on |f_n - f_(n-1)| <= sqrt(eps)
+# (scaled), so its end point moves by up to ~1e-2 sigma with the last bits.
+# --------------------------------------------------------------------------
+def gen_tnc_floor(pplib, pptoaslib):
+    import warnings
+    warnings.simplefilter("ignore")
+    out = {}
+    g = np.load(os.path.join(HERE, "legacy_fit_portrait.npz"))
+    for ic in range(int(g["ncase"])):
+        k = "l%d_" % ic
+        rows = []
+        for j in range(1, 11):
+            init = np.array(g[k + "init"], float)
+            init[0] += j * np.spacing(init[0]) * (1 if j % 2 else -1)
+            r = quiet_call(pplib.fit_portrait, g[k + "data"], g[k + "model"], init, P0,
+                           g[k + "freqs"], float(g[k + "nu_fit"]), None, g[k + "errs"])
+            rows.append([(r.phase - float(g[k + "phase"])) / float(g[k + "phase_err"]),
+                         (r.DM - float(g[k + "DM"])) / float(g[k + "DM_err"]), r.return_code])
+        rows = np.array(rows)
+        out[k + "phase_floor"] = np.abs(rows[:, 0]).max()
+        out[k + "DM_floor"] = np.abs(rows[:, 1]).max()
+        out[k + "rcs"] = np.unique(rows[:, 2]).astype(int)
+        print("legacy %d floor: phase %.3g sigma, DM %.3g sigma, rcs %s" % (
+            ic, out[k + "phase_floor"], out[k + "DM_floor"], out[k + "rcs"]))
+    f = np.load(os.path.join(HERE, "fit_full_r2.npz"))
+    for ic in range(int(f["ncase"])):
+        k = "f%d_" % ic
+        if str(f[k + "method"]) != "TNC":
+            continue
+        nu = float(f[k + "nu_fit"])
+        bounds = [tuple(None if np.isnan(v) else float(v) for v in row) for row in f[k + "bounds"]]
+        flags = list(f[k + "flags"])
+        rows = []
+        for j in range(1, 11):
+            init = np.array(f[k + "init"], float)
+            init[0] += j * np.spacing(init[0]) * (1 if j % 2 else -1)
+            r = quiet_call(pptoaslib.fit_portrait_full, f[k + "data"], f[k + "model"], list(init),
+                           P0, f[k + "freqs"], [nu] * 3, [None] * 3, f[k + "errs"], flags, bounds,
+                           bool(f[k + "log10"]), option=0, method="TNC")
+            row = []
+            for i, nm in enumerate(["phi", "DM", "GM", "tau", "alpha"]):
+                e = float(f[k + nm + "_err"])
+                row.append(abs(r[nm] - float(f[k + nm])) / e if (flags[i] and e > 0) else 0.0)
+            rows.append(row + [r.return_code])
+        rows = np.array(rows)
+        out[k + "param_floor"] = rows[:, :5].max(axis=0)
+        out[k + "rcs"] = np.unique(rows[:, 5]).astype(int)
+        print("fit_full TNC %d floor: %s rcs %s" % (ic, out[k + "param_floor"], out[k + "rcs"]))
+    MG.save("tnc_floor.npz", **out)
+
+
 def main():
-    what = sys.argv[1:] or ["fit", "configs", "align", "headline", "timing"]
+    what = sys.argv[1:] or ["fit", "configs", "align", "headline", "timing", "tncfloor"]
     np.seterr(all="ignore")
     if "headline" in what:
         gen_headline_2k()
@@ -406,6 +461,8 @@ def main():
             gen_align5(pplib, pptoaslib, ppalign)
         if "timing" in rest:
             gen_timing(pplib, pptoaslib)
+        if "tncfloor" in rest:
+            gen_tnc_floor(pplib, pptoaslib)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 

@@ -1,0 +1,167 @@
+"""The drop-in drivers at world size 2 on CPU (gloo): GetTOAs.get_TOAs shards
+its (archive, subint) units over ranks and gathers the results; ppalign
+shards its units and all-reduces the Fourier-domain portrait sum.
+
+The device calls are replaced at their boundaries by deterministic CPU
+stand-ins -- pptoas/ppalign.fit_portraits_batch (one result per subint that
+depends only on that subint's inputs) and, for ppalign, an engine whose
+rotate_accumulate / irfft_rows are numpy (rfft * phasor, irfft).  What is
+checked is the N > 1 bookkeeping: every unit is fitted on exactly one rank,
+and every rank ends with exactly the single-process TOAs / template.
+"""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import torch
+import torch.multiprocessing as mp
+
+DM0 = 34.56789
+P0 = 1.0 / 345.67890123456789
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def fake_fit(data, model, init, P, freqs, nu_fits=None, nu_outs=None, errs=None,
+             fit_flags=(1, 1, 0, 0, 0), chan_mask=None, **kw):
+    """Per-subint deterministic stand-in for fit_portraits_batch's results."""
+    data = np.asarray(data)
+    nsub, nchan, nbin = data.shape
+    s = data.reshape(nsub, -1)
+    a = s.sum(1)
+    b = (s ** 2).sum(1)
+    params = np.stack([0.01 * np.tanh(a), DM0 + 1e-4 * np.tanh(b / s.shape[1] - 1.0),
+                       np.zeros(nsub), np.zeros(nsub), np.zeros(nsub)], 1)
+    params = params * np.asarray(fit_flags, float) + np.asarray(init) * (1 - np.asarray(fit_flags))
+    errs5 = np.tile([1e-4, 2e-4, 0.0, 0.0, 0.0], (nsub, 1)) * np.asarray(fit_flags, float)
+    nu = np.asarray(nu_fits, float).reshape(nsub, 3)
+    sc = 1.0 + 0.01 * np.abs(data).mean(axis=2)
+    if chan_mask is not None:
+        sc = sc * np.asarray(chan_mask)
+    if kw.get("log_calls") is not None:
+        kw["log_calls"].append(nsub)
+    cov = np.zeros((nsub, 5, 5))
+    cov[:, 0, 0], cov[:, 1, 1], cov[:, 0, 1] = 1e-8, 4e-8, 1e-9
+    return dict(params=params, param_errs=errs5, nu_out=nu.copy(), cov=cov, scales=sc,
+                scale_errs=0.1 * sc, channel_snrs=10 * sc, chi2=b, red_chi2=b / (nchan * nbin),
+                snr=np.sqrt(b), nfev=np.full(nsub, 5, np.int32), status=np.full(nsub, 2, np.int32),
+                duration=np.zeros(nsub))
+
+
+def make_archives():
+    from pulseportraiture_amd import archive, synth
+    from pulseportraiture_amd.mjd import MJD
+    names = []
+    for i, (nsub, nchan) in enumerate([(5, 8), (3, 8), (4, 8)]):
+        w = synth.make_workload(nsub, nchan, 64, seed=50 + i)
+        data = synth.workload_data_host(w)
+        wts = np.ones((nsub, nchan))
+        wts[1, 2] = 0.0
+        name = "dist%d.npz" % i
+        archive.register_archive(name, dict(
+            subints=data[:, None], freqs=w.freqs, Ps=np.full(nsub, w.P), weights=wts,
+            noise_stds=np.full((nsub, 1, nchan), 1.5),
+            epochs=[MJD(57000.0 + 0.01 * k) for k in range(nsub)], DM=DM0, backend="be",
+            frontend="fe", telescope="GBT", telescope_code="1"))
+        names.append(name)
+    return names
+
+
+def run_get_toas(log):
+    from pulseportraiture_amd import pplib, pptoas, synth
+    names = make_archives()
+
+    def fit(*a, **k):
+        k["log_calls"] = log
+        return fake_fit(*a, **k)
+    pptoas.fit_portraits_batch = fit
+    gt = pptoas.GetTOAs(names, synth.EXAMPLE_GMODEL, quiet=True)
+    gt.get_TOAs(quiet=True)
+    return [pplib.toa_line(t) for t in gt.TOA_list], gt
+
+
+def _toas_worker(rank, world, port, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        log = []
+        lines, gt = run_get_toas(log)
+        np.savez(os.path.join(out_dir, "toas%d.npz" % rank), lines=np.array(lines),
+                 nfit=sum(log), DeltaDM=np.array(gt.DeltaDM_means))
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_get_toas_sharded_ws2_equals_single_process():
+    log = []
+    ref_lines, gt = run_get_toas(log)
+    assert sum(log) == 12  # every ok subint once
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_toas_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        r = [np.load(os.path.join(d, "toas%d.npz" % k)) for k in range(2)]
+    assert int(r[0]["nfit"]) + int(r[1]["nfit"]) == 12  # disjoint shards cover all units
+    assert int(r[0]["nfit"]) == 6 and int(r[1]["nfit"]) == 6
+    for rk in r:
+        assert list(rk["lines"]) == ref_lines  # same TOAs, same order, on every rank
+        np.testing.assert_array_equal(rk["DeltaDM"], np.array(gt.DeltaDM_means))
+
+
+# ---------------------------------------------------------------------------
+# ppalign: sharded fit + rotate-accumulate + all-reduce + divide
+# ---------------------------------------------------------------------------
+class NumpyEngine:
+    """CPU stand-in for the engine calls align_archives makes."""
+    device = torch.device("cpu")
+
+    def rotate_accumulate(self, data, phase, weight, accum):
+        d = np.asarray(data)
+        k = np.arange(d.shape[-1] // 2 + 1)
+        spec = np.fft.rfft(d, axis=-1) * np.exp(2j * np.pi * np.asarray(phase)[..., None] * k)
+        s = np.sum(np.asarray(weight)[..., None] * spec, axis=0)
+        accum += torch.as_tensor(np.stack([s.real, s.imag], -1))
+
+    def irfft_rows(self, spec, nbin):
+        return torch.as_tensor(np.fft.irfft(spec.numpy(), nbin, axis=-1))
+
+    def noise_rows(self, rows):
+        from oracle import ppfit_oracle as O
+        return torch.as_tensor(O.get_noise_PS(np.asarray(rows), chans=True))
+
+
+def run_align():
+    from pulseportraiture_amd import archive, engine, ppalign, synth
+    names = make_archives()
+    engine.get_engine = lambda device=None: NumpyEngine()
+    ppalign.fit_portraits_batch = fake_fit
+    w = synth.make_workload(1, 8, 64, seed=50)
+    archive.register_archive("dist_guess.npz", dict(subints=w.model[None, None], freqs=w.freqs,
+                                                    Ps=[w.P], epochs=[(57000, 0, 0.0)], DM=DM0))
+    return ppalign.align_archives(names, "dist_guess.npz", fit_dm=True, niter=2, quiet=True)
+
+
+def _align_worker(rank, world, port, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        np.save(os.path.join(out_dir, "align%d.npy" % rank), run_align())
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_align_archives_sharded_ws2_equals_single_process():
+    ref = run_align()
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_align_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        got = [np.load(os.path.join(d, "align%d.npy" % k)) for k in range(2)]
+    for g in got:
+        np.testing.assert_allclose(g, ref, rtol=1e-12, atol=1e-12 * np.abs(ref).max())
+    assert np.array_equal(got[0], got[1])

@@ -256,16 +256,20 @@ def test_fit_full_r2_tnc(eng, golden, ic):
         assert {rc, ref_rc} <= CONVERGED, (rc, ref_rc)
     if ref_rc == 3:
         assert rc == 3 and int(r["nfev"][0]) == int(f[k + "nfeval"])
-    tol = 1e-2 if ref_rc == 3 else 1e-3
+    # TNC stops on |f_n - f_(n-1)| <= sqrt(eps) (scaled): the reference's own
+    # end point moves when its start moves by a few ulps (tnc_floor.npz).  The
+    # bar is north_star's 1e-3 sigma or twice that measured floor.
+    floor = golden("tnc_floor.npz")[k + "param_floor"]
+    tol = np.maximum(1e-3, 2.0 * floor)
     flags = [int(v) for v in f[k + "flags"]]
     ref = {key: float(f[k + key]) for key in ["phi", "phi_err", "nu_DM", "nu_GM"]}
     p = r["params"][0]
     assert phase_gap(p[0], p[1], p[2], r["nu_out"][0][0], r["nu_out"][0][1], ref,
-                     float(f["P"])) <= tol
+                     float(f["P"])) <= tol[0]
     for i, nm in enumerate(["DM", "GM", "tau", "alpha"], start=1):
         if flags[i]:
             sig = float(f[k + nm + "_err"])
-            assert abs(p[i] - float(f[k + nm])) <= tol * sig, (nm, p[i], float(f[k + nm]), sig)
+            assert abs(p[i] - float(f[k + nm])) <= tol[i] * sig, (nm, p[i], float(f[k + nm]), sig)
             assert r["param_errs"][0][i] == pytest.approx(sig, rel=1e-3 if ref_rc == 3 else 1e-5)
     assert r["red_chi2"][0] == pytest.approx(float(f[k + "red_chi2"]), rel=1e-6)
     print("TNC case %d: status %d (reference %d), nfev %d (reference %d)" % (
@@ -284,11 +288,17 @@ def test_legacy_fit_portrait_tnc(eng, golden, ic):
     ref_rc = int(g[k + "return_code"])
     if r.return_code != ref_rc:
         assert {r.return_code, ref_rc} <= CONVERGED, (r.return_code, ref_rc)
-    assert abs(r.phase - float(g[k + "phase"])) <= 1e-3 * float(g[k + "phase_err"])
-    assert abs(r.DM - float(g[k + "DM"])) <= 1e-3 * float(g[k + "DM_err"])
-    for key in ["phase_err", "DM_err", "nu_ref", "red_chi2", "snr"]:
+    fl = golden("tnc_floor.npz")  # the reference's own ulp-restart spread
+    tphi = max(1e-3, 2.0 * float(fl[k + "phase_floor"]))
+    tdm = max(1e-3, 2.0 * float(fl[k + "DM_floor"]))
+    dphi = abs(r.phase - float(g[k + "phase"])) / float(g[k + "phase_err"])
+    assert dphi <= tphi, (dphi, tphi)
+    assert abs(r.DM - float(g[k + "DM"])) <= tdm * float(g[k + "DM_err"])
+    for key in ["phase_err", "DM_err", "red_chi2", "snr"]:
         assert r[key] == pytest.approx(float(g[k + key]), rel=1e-6), key
-    assert r.covariance == pytest.approx(float(g[k + "covariance"]), rel=1e-5)
+    assert r.nu_ref == pytest.approx(float(g[k + "nu_ref"]), rel=1e-7)
+    c = float(g[k + "covariance"])  # ~0 at the zero-covariance frequency
+    assert abs(r.covariance - c) <= 1e-6 * float(g[k + "phase_err"]) * float(g[k + "DM_err"])
     np.testing.assert_allclose(r.scales, g[k + "scales"], rtol=1e-6)
     np.testing.assert_allclose(r.scale_errs, g[k + "scale_errs"], rtol=1e-8)
     print("legacy TNC %d: status %d (reference %d), nfev %d (reference %d)" % (
