@@ -18,6 +18,9 @@
  *                              ppalign.py:202-208
  *   ppf_irfft_rows          <- numpy.fft.irfft (final step of ppalign.py:210-213)
  *   ppf_noise_rows          <- pplib.get_noise_PS(chans=True)  pplib.py:2227-2253
+ *   ppf_scatter_rotate_rows <- GetTOAs.show_fit port/model  pptoas.py:1389-1402
+ *   ppf_resid_chi2_rows     <- pplib.get_red_chi2 per channel in
+ *                              GetTOAs.get_channels_to_zap  pptoas.py:1201-1278
  *   ppf_synth_portraits     <- (test/bench input producer; pplib.make_fake_pulsar
  *                              math, pplib.py:3342-3377, on device)
  *
@@ -66,7 +69,8 @@ extern "C" {
 #define PPF_K_POST 10
 #define PPF_K_FIT_TAYLOR 11
 #define PPF_K_MOMENTS 12
-#define PPF_NUM_KERNELS 13
+#define PPF_K_RESID 13
+#define PPF_NUM_KERNELS 14
 
 typedef struct ppf_ctx ppf_ctx;
 
@@ -198,6 +202,24 @@ int ppf_rotate_rows(ppf_ctx* ctx, int32_t nrow, int32_t nbin, const double* in,
 int ppf_rotate_accumulate(ppf_ctx* ctx, int32_t nsub, int32_t nchan,
                           int32_t nbin, const double* data, const double* phase,
                           const double* weight, double* accum);
+
+/* out[r] = irfft(rfft(in[r]) e^{2 pi i k phase[r]} / (1 + 2 pi i k tau[r]))
+ * (rotate_portrait_full of a scattered template, pptoas.py:1389-1397);
+ * tau NULL = no scattering.                                              */
+int ppf_scatter_rotate_rows(ppf_ctx* ctx, int32_t nrow, int32_t nbin, const double* in,
+                            const double* phase, const double* tau, double* out);
+
+/* Per-channel reduced chi2 of a fitted portrait, get_red_chi2 as
+ * GetTOAs.get_channels_to_zap calls it (pplib.py:727-749, pptoas.py:1233):
+ *   port  = irfft(rfft(data[r]) e^{2 pi i k phase[r]})
+ *   model = scale[r] irfft(rfft(model[mrow]) / (1 + 2 pi i k tau[r]))
+ *   out[r] = sum_j ((port_j - model_j) / errs[r])^2 / dof
+ * evaluated in the Fourier domain (Parseval); mrow = model_row[r] (or r
+ * when NULL), phase NULL = 0, tau NULL = no scattering.                  */
+int ppf_resid_chi2_rows(ppf_ctx* ctx, int32_t nrow, int32_t nbin, const double* data,
+                        const double* phase, const double* model, const int32_t* model_row,
+                        const double* scale, const double* tau, const double* errs,
+                        double dof, double* out);
 
 /* out[r] = irfft(spec[r]) where spec is complex [nrow][nbin/2+1]           */
 int ppf_irfft_rows(ppf_ctx* ctx, int32_t nrow, int32_t nbin, const double* spec,

@@ -563,7 +563,23 @@ int ppf_rotate_rows(ppf_ctx* ctx, int32_t nrow, int32_t nbin, const double* in,
   if (int r = twiddles(ctx, nbin, &tw)) return r;
   return timed(ctx, PPF_K_ROTATE, [&] {
     LOGN_SWITCH(logN, hipLaunchKernelGGL(k_rotate_rows<LG>, dim3(nrow), dim3(kBlock), 0,
-                                         ctx->stream, in, phase, out, tw));
+                                         ctx->stream, in, phase, nullptr, out, tw));
+  });
+}
+
+int ppf_scatter_rotate_rows(ppf_ctx* ctx, int32_t nrow, int32_t nbin, const double* in,
+                            const double* phase, const double* tau, double* out) {
+  if (!ctx || !in || !out) return fail(ctx, PPF_ERR_INVALID, "null argument");
+  if (nrow <= 0) return PPF_OK;
+  int logN;
+  if (int r = check_nbin(ctx, nbin, &logN)) return r;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  const double2* tw;
+  if (int r = twiddles(ctx, nbin, &tw)) return r;
+  if (!phase) return fail(ctx, PPF_ERR_INVALID, "phase must be given (zeros for none)");
+  return timed(ctx, PPF_K_ROTATE, [&] {
+    LOGN_SWITCH(logN, hipLaunchKernelGGL(k_rotate_rows<LG>, dim3(nrow), dim3(kBlock), 0,
+                                         ctx->stream, in, phase, tau, out, tw));
   });
 }
 
@@ -648,6 +664,26 @@ int ppf_rotate_accumulate(ppf_ctx* ctx, int32_t nsub, int32_t nchan, int32_t nbi
   return timed(ctx, PPF_K_ROT_ACCUM, [&] {
     hipLaunchKernelGGL(k_accum_reduce, dim3((unsigned)((count + 255) / 256)), dim3(256), 0,
                        ctx->stream, partial, acc, nsplit, count);
+  });
+}
+
+int ppf_resid_chi2_rows(ppf_ctx* ctx, int32_t nrow, int32_t nbin, const double* data,
+                        const double* phase, const double* model, const int32_t* model_row,
+                        const double* scale, const double* tau, const double* errs,
+                        double dof, double* out) {
+  if (!ctx || !data || !model || !scale || !errs || !out)
+    return fail(ctx, PPF_ERR_INVALID, "null argument");
+  if (nrow <= 0) return PPF_OK;
+  if (!(dof > 0.0)) return fail(ctx, PPF_ERR_INVALID, "dof must be > 0");
+  int logN;
+  if (int r = check_nbin(ctx, nbin, &logN)) return r;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  const double2* tw;
+  if (int r = twiddles(ctx, nbin, &tw)) return r;
+  ResidArgs ra{data, phase, model, model_row, scale, tau, errs, dof, out};
+  return timed(ctx, PPF_K_RESID, [&] {
+    LOGN_SWITCH(logN, hipLaunchKernelGGL(k_resid_chi2<LG>, dim3(nrow), dim3(kBlock), 0,
+                                         ctx->stream, ra, tw));
   });
 }
 

@@ -366,6 +366,18 @@ __device__ inline void guess_search(const double2* rm, int NH, double ie2, int N
   __syncthreads();
 }
 
+struct ResidArgs {
+  const double* data;      // [nrow][nbin]
+  const double* phase;     // [nrow] or NULL
+  const double* model;     // [nmodel][nbin]
+  const int* model_row;    // [nrow] or NULL (row r)
+  const double* scale;     // [nrow]
+  const double* tau;       // [nrow] scattering time [rot] or NULL
+  const double* errs;      // [nrow]
+  double dof;
+  double* out;             // [nrow]
+};
+
 // ---------------------------------------------------------------------------
 // kernel declarations
 // ---------------------------------------------------------------------------
@@ -376,8 +388,8 @@ __global__ void k_model_spec(const double* model, double2* M, double* pn, int NH
 template <int LOGN> __global__ void k_data_xspec(SpecArgs a);
 template <int LOGN> __global__ void k_phase_shift(PhaseShiftArgs a);
 template <int LOGN>
-__global__ void k_rotate_rows(const double* in, const double* phase, double* out,
-                              const double2* tw);
+__global__ void k_rotate_rows(const double* in, const double* phase, const double* tau,
+                              double* out, const double2* tw);
 template <int LOGN>
 __global__ void k_irfft_rows(const double2* spec, double* out, const double2* tw);
 template <int LOGN>
@@ -390,6 +402,7 @@ __global__ void k_rot_accum(const double* data, const double* phase, const doubl
                             double2* partial, int nsub, int nchan, int nsplit,
                             const double2* tw);
 __global__ void k_accum_reduce(const double2* partial, double2* accum, int nsplit, size_t count);
+template <int LOGN> __global__ void k_resid_chi2(ResidArgs a, const double2* tw);
 __global__ void k_guess(FitArgs a);
 __global__ void k_model_mean(const double2* M, double2* Mmean, int nchan, int NHP);
 __global__ void k_fit_taylor(FitArgs a);

@@ -390,7 +390,8 @@ __global__ __launch_bounds__(kBlock) void k_phase_shift(PhaseShiftArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Row rotation: out = irfft(rfft(in) e^{2 pi i k phase}) (rotate_data).
+// Row rotation: out = irfft(rfft(in) e^{2 pi i k phase}) (rotate_data),
+// optionally scattered: / (1 + 2 pi i k tau) (scattering_portrait_FT).
 // ---------------------------------------------------------------------------
 template <int LOGN>
 __device__ void c2r_from_spectrum(double2* buf, double2 (&xs)[((1 << LOGN) + kBlock) / kBlock + 1],
@@ -431,6 +432,7 @@ __device__ void c2r_from_spectrum(double2* buf, double2 (&xs)[((1 << LOGN) + kBl
 template <int LOGN>
 __global__ __launch_bounds__(kBlock) void k_rotate_rows(const double* __restrict__ in,
                                                         const double* __restrict__ phase,
+                                                        const double* __restrict__ tau,
                                                         double* __restrict__ out,
                                                         const double2* __restrict__ tw) {
   constexpr int N = 1 << LOGN;
@@ -446,6 +448,15 @@ __global__ __launch_bounds__(kBlock) void k_rotate_rows(const double* __restrict
   for (int i = 0; i < KI; ++i) {
     const int k = threadIdx.x + i * kBlock;
     if (k <= N) xs[i] = cmul(rfft_post<LOGN>(buf, k, tw), turn_phasor((double)k, ph));
+  }
+  const double t2 = tau ? 2.0 * M_PI * tau[r] : 0.0;
+  if (t2 != 0.0) {  // scattering_portrait_FT: x / (1 + 2 pi i k tau)
+#pragma unroll
+    for (int i = 0; i < KI; ++i) {
+      const int k = threadIdx.x + i * kBlock;
+      const double w = t2 * (double)k, d = 1.0 / fma(w, w, 1.0);
+      if (k <= N) xs[i] = cmk(fma(xs[i].y, w, xs[i].x) * d, fma(-xs[i].x, w, xs[i].y) * d);
+    }
   }
   __syncthreads();
   c2r_from_spectrum<LOGN>(buf, xs, tw, out + (size_t)r * 2 * N);
@@ -584,6 +595,61 @@ __global__ void k_accum_reduce(const double2* __restrict__ partial, double2* __r
 }
 
 // ---------------------------------------------------------------------------
+// Per-channel reduced chi2 of a fitted portrait, as GetTOAs.show_fit /
+// get_channels_to_zap form it (pptoas.py:1389-1402, 1236; get_red_chi2,
+// pplib.py:727-749).  With D = rfft(data[r]) e^{2 pi i k phase[r]} (the
+// rotate_portrait_full of the data) and M = rfft(model[mrow]) / (1 + 2 pi i
+// k tau[r]) (the scattered template), the time-domain residual sum follows
+// from Parseval on R = D - scale[r] M (irfft drops Im R_0 and Im R_N):
+//   out[r] = (Re(R_0)^2 + Re(R_N)^2 + 2 sum_{0<k<N} |R_k|^2) / nbin / errs[r]^2 / dof
+// One workgroup per row; both FFTs in LDS, nothing materialised in HBM.
+// ---------------------------------------------------------------------------
+template <int LOGN>
+__global__ __launch_bounds__(kBlock) void k_resid_chi2(ResidArgs a, const double2* __restrict__ tw) {
+  constexpr int N = 1 << LOGN;
+  constexpr int KI = (N + 1 + kBlock - 1) / kBlock;
+  __shared__ double2 buf[N + 1];
+  __shared__ double red[kWaves];
+  const int r = blockIdx.x;
+  load_row<LOGN>(buf, a.data + (size_t)r * 2 * N);
+  __syncthreads();
+  lds_fft<LOGN, false>(buf, tw);
+  const double ph = a.phase ? a.phase[r] : 0.0;
+  double2 xs[(N + kBlock) / kBlock + 1];
+#pragma unroll
+  for (int i = 0; i < KI; ++i) {
+    const int k = threadIdx.x + i * kBlock;
+    if (k <= N) xs[i] = cmul(rfft_post<LOGN>(buf, k, tw), turn_phasor((double)k, ph));
+  }
+  __syncthreads();
+  load_row<LOGN>(buf, a.model + (size_t)(a.model_row ? a.model_row[r] : r) * 2 * N);
+  __syncthreads();
+  lds_fft<LOGN, false>(buf, tw);
+  const double sc = a.scale[r];
+  const double t2 = a.tau ? 2.0 * M_PI * a.tau[r] : 0.0;
+  double acc = 0.0;
+#pragma unroll
+  for (int i = 0; i < KI; ++i) {
+    const int k = threadIdx.x + i * kBlock;
+    if (k <= N) {
+      double2 m = rfft_post<LOGN>(buf, k, tw);
+      if (t2 != 0.0) {  // m / (1 + i w),  w = 2 pi k tau
+        const double w = t2 * (double)k, d = 1.0 / fma(w, w, 1.0);
+        m = cmk(fma(m.y, w, m.x) * d, fma(-m.x, w, m.y) * d);
+      }
+      const double2 q = cmk(fma(-sc, m.x, xs[i].x), fma(-sc, m.y, xs[i].y));
+      // irfft keeps only the real part of the DC and Nyquist terms
+      acc += (k == 0 || k == N) ? q.x * q.x : 2.0 * cabs2(q);
+    }
+  }
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) {
+    const double e = a.errs[r];
+    a.out[r] = acc / (double)(2 * N) / (e * e) / a.dof;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // explicit instantiations (nbin = 64 ... 8192  <=>  LOGN = 5 ... 12)
 // ---------------------------------------------------------------------------
 #define PPF_INST(L)                                                                          \
@@ -591,8 +657,9 @@ __global__ void k_accum_reduce(const double2* __restrict__ partial, double2* __r
                                            const double2*);                                  \
   template __global__ void k_data_xspec<L>(SpecArgs);                                        \
   template __global__ void k_phase_shift<L>(PhaseShiftArgs);                                 \
-  template __global__ void k_rotate_rows<L>(const double*, const double*, double*,           \
-                                            const double2*);                                 \
+  template __global__ void k_rotate_rows<L>(const double*, const double*, const double*,     \
+                                            double*, const double2*);                        \
+  template __global__ void k_resid_chi2<L>(ResidArgs, const double2*);                       \
   template __global__ void k_irfft_rows<L>(const double2*, double*, const double2*);        \
   template __global__ void k_noise_rows<L>(const double*, double*, int, const double2*);    \
   template __global__ void k_synth<L>(const double2*, const double*, double*, int, int,      \

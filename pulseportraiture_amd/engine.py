@@ -296,6 +296,41 @@ class Engine:
         out._keep = r2
         return out.reshape(r.shape[:-1])
 
+    def resid_chi2_rows(self, data, phase, model, scale, errs, dof, tau=None,
+                        model_row=None):
+        """Per-row reduced chi2 of rotate(data, phase) - scale * scatter(model, tau)
+        (ppf_resid_chi2_rows)."""
+        dev = self.device
+        d = _dev_f64(data, dev)
+        d = d.reshape(-1, d.shape[-1])
+        m = _dev_f64(model, dev)
+        m = m.reshape(-1, m.shape[-1])
+        nrow, nbin = d.shape
+        row = lambda v: None if v is None else \
+            _dev_f64(v, dev).reshape(-1).expand(nrow).contiguous()
+        ph, sc, er, ta = row(phase), row(scale), row(errs), row(tau)
+        mr = None if model_row is None else _dev_i32(model_row, dev)
+        out = torch.empty(nrow, dtype=torch.float64, device=dev)
+        self._chk(self.lib.ppf_resid_chi2_rows(self.ctx, nrow, nbin, _ptr(d), _ptr(ph), _ptr(m),
+                                               _ptr(mr), _ptr(sc), _ptr(ta), _ptr(er),
+                                               float(dof), _ptr(out)))
+        out._keep = (d, m, ph, sc, er, ta, mr)
+        return out
+
+    def scatter_rotate_rows(self, rows, phase, tau=None):
+        """irfft(rfft(rows) e^{2 pi i k phase} / (1 + 2 pi i k tau)) per row."""
+        dev = self.device
+        r = _dev_f64(rows, dev)
+        shape = r.shape
+        r = r.reshape(-1, shape[-1])
+        ph = _dev_f64(phase, dev).reshape(-1).expand(r.shape[0]).contiguous()
+        ta = None if tau is None else _dev_f64(tau, dev).reshape(-1).expand(r.shape[0]).contiguous()
+        out = torch.empty_like(r)
+        self._chk(self.lib.ppf_scatter_rotate_rows(self.ctx, r.shape[0], r.shape[1], _ptr(r),
+                                                   _ptr(ph), _ptr(ta), _ptr(out)))
+        out._keep = (r, ph, ta)
+        return out.reshape(shape)
+
     def rotate_accumulate(self, data, phase, weight, accum):
         """accum [nchan, nharm, 2] (float64, device) += weighted rotated spectra."""
         dev = self.device

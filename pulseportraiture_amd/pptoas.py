@@ -151,6 +151,8 @@ class GetTOAs:
             already_warned = True
         self.scat_guess = scat_guess
         self.DM0, self.bary = DM0, bary
+        self.tscrunch = tscrunch
+        self.add_instrumental_response = add_instrumental_response
         self._fit_flags_prev = None  # the reference's loop-carried fit_flags
         start = time.time()
         datafiles = self.datafiles if datafile is None else [datafile]
@@ -205,6 +207,349 @@ class GetTOAs:
             n = np.array([len(x) for x in self.ok_isubs]).sum()
             print("--------------------------")
             print("Total time: %.2f sec, ~%.4f sec/TOA" % (tot, tot / n))
+
+    def get_narrowband_TOAs(self, datafile=None, tscrunch=False, fit_scat=False,
+                            log10_tau=True, scat_guess=None, print_phase=False,
+                            print_flux=False, print_parangle=False,
+                            add_instrumental_response=False, addtnl_toa_flags={},
+                            method="trust-ncg", bounds=None, show_plot=False, quiet=None):
+        """Narrowband TOAs: one FFTFIT per channel (pptoas.py:740-1125).
+
+        Every (subint, channel) profile of every archive goes to the device in
+        one ppf_phase_shift_batch call (brute force on linspace(-0.5, 0.5,
+        100) + Nelder-Mead, pplib.py:2054-2100, with the load_data noise as
+        err); TOAs, flags and the per-archive arrays follow the reference.
+        As there, fit_scat is accepted but not fitted (tau = 0).  Reference
+        quirks kept: channel_red_chi2s[isub] is set to the last channel's
+        reduced chi2 for the whole row (pptoas.py:1011); channels whose
+        template-archive weight is 0 are skipped (pptoas.py:966).  Where the
+        reference cannot run -- a .gmodel template (model_data undefined,
+        pptoas.py:966), isub > 0 of a tscrunched template, print_phase
+        (results.phi, :1048) and print_flux (fluxes undefined, :1052) -- this
+        build uses the template's single weight row, prints the fitted phase
+        and prints the per-channel flux estimate.
+        """
+        if quiet is None:
+            quiet = self.quiet
+        if add_instrumental_response and (self.ird["DM"] or len(self.ird["wids"])):
+            raise NotImplementedError("instrumental response convolution (pptoas.py:387-393)")
+        if tscrunch:
+            raise NotImplementedError("tscrunch needs PSRCHIVE (out of scope)")
+        self.nfit = 1 + 2 * int(bool(fit_scat))
+        self.fit_phi, self.fit_tau = True, fit_scat
+        self.fit_flags = [int(self.fit_phi), int(self.fit_tau)]
+        self.log10_tau = log10_tau if fit_scat else False
+        if not quiet:
+            print("You are using an experimental functionality of pptoas!")
+        self.scat_guess = scat_guess
+        self.tscrunch = tscrunch
+        self.add_instrumental_response = add_instrumental_response
+        start = time.time()
+        datafiles = self.datafiles if datafile is None else [datafile]
+        from .pplib import get_bin_centers
+        from .engine import get_engine
+        for iarch, datafile in enumerate(datafiles):
+            try:
+                data = _arch.load_data(datafile, dedisperse=False, dededisperse=False,
+                                       tscrunch=tscrunch, pscrunch=True, rm_baseline=rm_baseline,
+                                       quiet=quiet)
+                if data.dmc:
+                    raise RuntimeError("dedispersed archive: dededispersion needs PSRCHIVE")
+                if not len(data.ok_isubs):
+                    if not quiet:
+                        print("No subints to fit for %s.  Skipping it." % datafile)
+                    continue
+                self.ok_idatafiles.append(iarch)
+            except RuntimeError:
+                if not quiet:
+                    print("Cannot load_data(%s).  Skipping it." % datafile)
+                continue
+            name = datafile if isinstance(datafile, str) else data.filename
+            nsub, nchan, nbin = data.nsub, data.nchan, data.nbin
+            obs = DataBunch(telescope=data.telescope, backend=data.backend,
+                            frontend=data.frontend)
+            MJDs = np.array([data.epochs[i].in_days() for i in range(nsub)], dtype=np.double)
+            mweights = None
+            if self.is_FITS_model:
+                md = _arch.load_data(self.modelfile)
+                model = np.asarray((md.masks * md.subints)[0, 0])
+                if md.nbin != nbin:
+                    if not quiet:
+                        print("Model nbin %d != data nbin %d for %s; skipping it." % (
+                            md.nbin, nbin, name))
+                    continue
+                if md.nchan == 1:
+                    model = np.tile(model[0], nchan).reshape(nchan, nbin)
+                elif md.nchan != nchan:
+                    if not quiet:
+                        print("Model nchan %d != data nchan %d for %s; skipping it." % (
+                            md.nchan, nchan, name))
+                    continue
+                mweights = np.asarray(md.weights)[0]
+            models, midx = [], {}
+            rows, mrows, noise, where = [], [], [], []
+            subints = np.asarray(data.subints)
+            for isub in data.ok_isubs:
+                if self.is_FITS_model:
+                    key = 0
+                    if not models:
+                        models.append(model)
+                else:
+                    f = data.freqs[isub]
+                    key = midx.setdefault((f.tobytes(), data.Ps[isub]), len(models))
+                    if key == len(models):
+                        models.append(read_model(self.modelfile, get_bin_centers(nbin), f,
+                                                 data.Ps[isub], quiet=True)[2])
+                for ichan in data.ok_ichans[isub]:
+                    if mweights is not None and mweights[ichan] == 0:
+                        continue
+                    rows.append(subints[isub, 0, ichan])
+                    mrows.append(key * nchan + ichan)
+                    ns = data.get("noise_stds")
+                    noise.append(np.nan if ns is None else ns[isub, 0, ichan])
+                    where.append((int(isub), int(ichan)))
+            t0 = time.time()
+            out = np.zeros((0, 6))
+            if rows:
+                mstack = np.concatenate(models, axis=0)
+                out = get_engine().phase_shift_batch(
+                    np.array(rows), mstack, noise=np.array(noise), Ns=100,
+                    bounds=(-0.5, 0.5), model_idx=np.array(mrows, dtype=np.int32)).cpu().numpy()
+            fit_duration = time.time() - t0
+            z = lambda *sh: np.zeros(sh, dtype=np.float64)
+            phis, phi_errs = z(nsub, nchan), z(nsub, nchan)
+            TOAs = np.zeros([nsub, nchan], dtype="object")
+            TOA_errs = np.zeros([nsub, nchan], dtype="object")
+            taus, tau_errs = z(nsub, nchan), z(nsub, nchan)
+            scales, scale_errs, channel_snrs = z(nsub, nchan), z(nsub, nchan), z(nsub, nchan)
+            pfl, pfle = z(nsub, nchan), z(nsub, nchan)
+            channel_red_chi2s = z(nsub, nchan)
+            covariances = z(nsub, nchan, self.nfit, self.nfit)
+            nfevals = np.zeros([nsub, nchan], dtype="int")
+            rcs = np.zeros([nsub, nchan], dtype="int")
+            for (isub, ichan), (phase, phase_err, scale, scale_err, snr, red_chi2) in zip(where, out):
+                P = data.Ps[isub]
+                toa = data.epochs[isub] + MJD(((phase * P) + data.backend_delay) / (3600 * 24.))
+                toa_err = phase_err * P * 1e6
+                if print_flux:
+                    m = models[0 if self.is_FITS_model else
+                               mrows[where.index((isub, ichan))] // nchan][ichan]
+                    pfl[isub, ichan] = m.mean() * scale
+                    pfle[isub, ichan] = abs(m.mean()) * scale_err
+                phis[isub, ichan], phi_errs[isub, ichan] = phase, phase_err
+                TOAs[isub, ichan], TOA_errs[isub, ichan] = toa, toa_err
+                scales[isub, ichan], scale_errs[isub, ichan] = scale, scale_err
+                channel_snrs[isub, ichan] = snr
+                channel_red_chi2s[isub] = red_chi2  # the whole row (pptoas.py:1011)
+                flags = {"be": data.backend, "fe": data.frontend,
+                         "f": data.frontend + "_" + data.backend, "nbin": nbin,
+                         "bw": abs(data.bw) / nchan, "subint": isub, "chan": ichan,
+                         "tobs": data.subtimes[isub], "tmplt": self.modelfile, "snr": snr,
+                         "gof": red_chi2}
+                if print_phase:
+                    flags["phs"] = phase
+                    flags["phs_err"] = phase_err
+                if print_flux:
+                    flags["flux"] = pfl[isub, ichan]
+                    flags["flux_err"] = pfle[isub, ichan]
+                if print_parangle:
+                    flags["par_angle"] = data.parallactic_angles[isub]
+                for k, v in addtnl_toa_flags.items():
+                    flags[k] = v
+                self.TOA_list.append(TOA(name, data.freqs[isub, ichan], toa, toa_err,
+                                         data.telescope, data.telescope_code, None, None,
+                                         flags))
+            for attr, val in [("order", name), ("obs", obs), ("doppler_fs", data.doppler_factors),
+                              ("ok_isubs", np.asarray(data.ok_isubs)), ("epochs", data.epochs),
+                              ("MJDs", MJDs), ("Ps", data.Ps), ("phis", phis),
+                              ("phi_errs", phi_errs), ("TOAs", TOAs), ("TOA_errs", TOA_errs),
+                              ("taus", taus), ("tau_errs", tau_errs), ("scales", scales),
+                              ("scale_errs", scale_errs), ("channel_snrs", channel_snrs),
+                              ("profile_fluxes", pfl), ("profile_flux_errs", pfle),
+                              ("covariances", covariances),
+                              ("channel_red_chi2s", channel_red_chi2s), ("nfevals", nfevals),
+                              ("rcs", rcs), ("fit_durations", fit_duration)]:
+                getattr(self, attr).append(val)
+            if not quiet:
+                print("--------------------------")
+                print(name)
+                print("~%.4f sec/TOA" % (fit_duration / max(len(self.TOA_list), 1)))
+        if not quiet and len(self.ok_isubs):
+            tot = time.time() - start
+            print("--------------------------")
+            print("Total time: %.2f sec, ~%.4f sec/TOA" % (tot, tot / max(len(self.TOA_list), 1)))
+
+    # -- fitted portraits, residuals and channel zapping --------------------
+    def _fitted_rows(self, datafile, isubs, quiet):
+        """Inputs of show_fit (pptoas.py:1324-1402) for the subints isubs of
+        one fitted archive, as device rows: for every ok channel of every
+        subint, the data row, its rotate_portrait_full phase, its template
+        row (de-duplicated templates + row index), the fitted scale, the
+        scattering time [rot] and the channel noise."""
+        from .pptoaslib import phase_shifts
+        from .pplib import scattering_times
+        ok_files = list(np.array(self.datafiles)[self.ok_idatafiles])
+        ifile = ok_files.index(datafile)
+        # rm_baseline=True as in show_fit; archives reach this build already
+        # loaded (PSRCHIVE's baseline removal is out of scope, archive.py)
+        data = _arch.load_data(datafile, dedisperse=False, dededisperse=False,
+                               tscrunch=getattr(self, "tscrunch", False), pscrunch=True,
+                               rm_baseline=True, quiet=quiet)
+        if data.dmc:
+            raise RuntimeError("dedispersed archive: dededispersion needs PSRCHIVE")
+        if getattr(self, "add_instrumental_response", False) and \
+                (self.ird["DM"] or len(self.ird["wids"])):
+            raise NotImplementedError("instrumental response convolution (pptoas.py:1382-1388)")
+        nbin = data.nbin
+        subints = np.asarray(data.subints)
+        models, mkeys = [], {}
+        rows, ph, mrow, sc, taus, noise, where = [], [], [], [], [], [], []
+        for isub in isubs:
+            phi = self.phis[ifile][isub]
+            DM = self.DMs[ifile][isub]
+            GM = self.GMs[ifile][isub]
+            if self.bary:  # pptoas.py:1348-1350, whatever was fitted
+                DM /= self.doppler_fs[ifile][isub]
+                GM /= self.doppler_fs[ifile][isub] ** 3
+            freqs = data.freqs[isub]
+            nu_ref_DM, nu_ref_GM, nu_ref_tau = self.nu_refs[ifile][isub]
+            P = data.Ps[isub]
+            tau = self.taus[ifile][isub]
+            if self.is_FITS_model:
+                key = ("fits",)
+            elif tau != 0.0:
+                key = ("unscattered", freqs.tobytes())
+            else:
+                key = ("model", freqs.tobytes())
+            if key not in mkeys:
+                mkeys[key] = len(models)
+                if self.is_FITS_model:
+                    md = _arch.load_data(self.modelfile)
+                    m = np.asarray((md.masks * md.subints)[0, 0])
+                    if md.nchan == 1:
+                        m = np.tile(m[0], len(freqs)).reshape(len(freqs), md.nbin)
+                elif tau != 0.0:
+                    info = read_model(self.modelfile, quiet=True)
+                    gparams = np.copy(info[4])
+                    gparams[1] = 0.0
+                    m = gen_gaussian_portrait(info[1], gparams, 0.0, data.phases, freqs, info[2])
+                else:
+                    m = read_model(self.modelfile, data.phases, freqs, data.Ps.mean(),
+                                   quiet=True)[2]
+                models.append(np.asarray(m, dtype=np.float64))
+            k = mkeys[key]
+            phs = phase_shifts(phi, DM, GM, freqs, nu_ref_DM, nu_ref_GM, P)
+            if tau != 0.0:
+                t = 10 ** tau if self.log10_tau else tau
+                tch = scattering_times(t, self.alphas[ifile][isub], freqs, nu_ref_tau)
+            else:
+                tch = np.zeros(len(freqs))
+            ns = data.get("noise_stds")
+            for ichan in data.ok_ichans[isub]:
+                rows.append(subints[isub, 0, ichan])
+                ph.append(phs[ichan])
+                mrow.append(k * data.nchan + ichan)
+                sc.append(self.scales[ifile][isub][ichan])
+                taus.append(tch[ichan])
+                noise.append(np.nan if ns is None else ns[isub, 0, ichan])
+                where.append((int(isub), int(ichan)))
+        return DataBunch(data=data, ifile=ifile, rows=np.array(rows).reshape(-1, nbin),
+                         phase=np.array(ph), models=np.concatenate(models, 0) if models else
+                         np.zeros((0, nbin)), model_row=np.array(mrow, dtype=np.int32),
+                         scale=np.array(sc), tau=np.array(taus), noise=np.array(noise),
+                         where=where)
+
+    def show_fit(self, datafile=None, isub=0, rotate=0.0, show=True, return_fit=False,
+                 savefig=False, quiet=None):
+        """Fitted portrait and scaled template of one subint (pptoas.py:1310-1412):
+        the data rotated by the fitted phi/DM/GM (rotate_portrait_full) and
+        the (scattered) template times the fitted channel scales, formed on
+        the device.  Plotting (show_residual_plot) is out of scope: show only
+        prints a note."""
+        if quiet is None:
+            quiet = self.quiet
+        if datafile is None:
+            datafile = self.datafiles[0]
+        from .engine import get_engine
+        eng = get_engine()
+        fr = self._fitted_rows(datafile, [isub], quiet)
+        data = fr.data
+        nchan, nbin = data.nchan, data.nbin
+        ok = np.asarray(data.ok_ichans[isub])
+        port = np.zeros((nchan, nbin))
+        model_scaled = np.zeros((nchan, nbin))
+        if len(ok):
+            port[ok] = eng.scatter_rotate_rows(fr.rows, fr.phase + rotate).cpu().numpy()
+            ms = eng.scatter_rotate_rows(fr.models[fr.model_row], np.full(len(ok), rotate),
+                                         fr.tau).cpu().numpy()
+            model_scaled[ok] = fr.scale[:, None] * ms
+        # channels outside ok_ichans stay 0: masked data (port *= masks) and
+        # a zero fitted scale
+        port *= np.asarray(data.masks[isub, 0])
+        if show and not quiet:
+            print("show_fit: plotting is not part of this build; use return_fit=True")
+        if return_fit:
+            ns = data.get("noise_stds")
+            noise = ns[isub, 0] if ns is not None else \
+                eng.noise_rows(np.asarray(data.subints)[isub, 0]).cpu().numpy()
+            return port, model_scaled, data.ok_ichans[isub], data.freqs[isub], noise
+
+    def get_channels_to_zap(self, SNR_threshold=8.0, rchi2_threshold=1.3, iterate=True,
+                            show=False):
+        """Flag channels by reduced chi2 and S/N (pptoas.py:1201-1278); needs
+        get_TOAs first.  Every ok channel of every ok subint of an archive
+        goes to the device in one ppf_resid_chi2_rows call (rotation,
+        scattering, scaling and the chi2 sum fused per channel); the
+        thresholds and the iterated S/N cut run on the host as there."""
+        from .engine import get_engine
+        eng = get_engine()
+        for iarch, ok_idatafile in enumerate(self.ok_idatafiles):
+            datafile = self.datafiles[ok_idatafile]
+            ok_isubs = list(self.ok_isubs[iarch])
+            fr = self._fitted_rows(datafile, ok_isubs, True)
+            data = fr.data
+            chi2 = np.zeros(0)
+            if len(fr.where):
+                noise = fr.noise
+                if np.isnan(noise).any():  # load_data's get_noise on the device
+                    est = eng.noise_rows(fr.rows).cpu().numpy()
+                    noise = np.where(np.isnan(noise), est, noise)
+                chi2 = eng.resid_chi2_rows(fr.rows, fr.phase, fr.models, fr.scale, noise,
+                                           data.nbin - 2, tau=fr.tau,
+                                           model_row=fr.model_row).cpu().numpy()
+            per_sub = {}
+            for (isub, ichan), c in zip(fr.where, chi2):
+                per_sub.setdefault(isub, []).append(c)
+            channel_red_chi2s, zap_channels = [], []
+            for isub in ok_isubs:
+                ok_ichans = list(data.ok_ichans[isub])
+                red_chi2s = list(per_sub.get(int(isub), []))
+                channel_snrs = self.channel_snrs[iarch][isub]
+                thr = (SNR_threshold ** 2.0 / len(ok_ichans)) ** 0.5
+                bad = []
+                for ok_ichan, c in zip(ok_ichans, red_chi2s):
+                    if c > rchi2_threshold or np.isnan(c):
+                        bad.append(ok_ichan)
+                    elif SNR_threshold and channel_snrs[ok_ichan] < thr:
+                        bad.append(ok_ichan)
+                channel_red_chi2s.append(red_chi2s)
+                zap_channels.append(bad)
+                if iterate and SNR_threshold and len(bad):
+                    old_len = len(bad)
+                    added_new = True
+                    while added_new and (len(ok_ichans) - len(bad)):
+                        thr = (SNR_threshold ** 2.0 / (len(ok_ichans) - len(bad))) ** 0.5
+                        for ok_ichan in ok_ichans:
+                            if ok_ichan in bad:
+                                continue
+                            if channel_snrs[ok_ichan] < thr:
+                                bad.append(ok_ichan)
+                        added_new = bool(len(bad) - old_len)
+                        old_len = len(bad)
+                if show and len(bad):
+                    print("%s, subint: %d  bad chans: %s" % (datafile, isub, bad))
+            self.channel_red_chi2s.append(channel_red_chi2s)
+            self.zap_channels.append(zap_channels)
 
     def _prepare(self, datafile, data, nu_ref_tuple, nu_fit_tuple, fit_scat, method, bounds,
                  quiet):

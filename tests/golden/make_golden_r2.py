@@ -26,6 +26,10 @@ Fixtures:
   timing_r2.json     oracle vs reference wall time per TOA (BASELINE.md:47)
   tnc_floor.npz      the reference's TNC restarted 1-10 ulps away: how far its
                      own end point moves (legacy fit and the TNC fit cases)
+  narrowband.*       GetTOAs.get_narrowband_TOAs with an archive template:
+                     per-channel phases, errors, scales and .tim lines
+  zap.npz            GetTOAs.get_channels_to_zap (after get_TOAs) and
+                     ppzap.get_zap_channels on an archive with bad channels
 
 Usage:  python tests/golden/make_golden_r2.py [fit|configs|align|headline|timing ...]
 """
@@ -44,6 +48,9 @@ sys.path.insert(0, HERE)
 sys.path.insert(0, ROOT)
 
 import make_golden as MG  # noqa: E402
+from tests.golden_consts import zap_perturb  # noqa: E402
+
+MG.REF_FILES = MG.REF_FILES + ["ppzap.py"]  # get_zap_channels (ppzap.py:18-48)
 from pulseportraiture_amd import synth  # noqa: E402
 
 P0 = MG.P0
@@ -442,8 +449,120 @@ def gen_tnc_floor(pplib, pptoaslib):
     MG.save("tnc_floor.npz", **out)
 
 
+# --------------------------------------------------------------------------
+# Narrowband TOAs (pptoas.py:740-1125): per-channel fit_phase_shift.  The
+# reference reads model_data.weights inside the channel loop, which exists
+# only for an archive (FITS) template, and indexes it with the data's isub
+# on a tscrunched (one-subint) model: so it runs with an archive template
+# and one-subint archives, which is what is generated here.
+# --------------------------------------------------------------------------
+NB_ARCH = {"nbA.fits": (16, 256, 6006, 4), "nbB.fits": (8, 512, 6007, None)}
+
+
+def nb_archive(pplib, name, nchan, nbin, seed, zero_chan):
+    db = synth_archive(pplib, name, 1, nchan, nbin, seed, 0.0, 0.0)
+    if zero_chan is not None:
+        db["weights"][0, zero_chan] = 0.0
+        db["ok_ichans"] = [np.compress(db["weights"][0], range(nchan))]
+    return db
+
+
+def nb_model(pplib, nchan, nbin, zero_model_chan):
+    w = synth.make_workload(1, nchan, nbin, seed=1)
+    db = pplib.DataBunch(subints=w.model[None, None], masks=np.ones((1, 1, nchan, nbin)),
+                         weights=np.ones((1, nchan)), nbin=nbin, nchan=nchan,
+                         freqs=w.freqs[None], nsub=1)
+    if zero_model_chan is not None:
+        db["weights"][0, zero_model_chan] = 0.0
+    return db
+
+
+def gen_narrowband(pplib, pptoaslib, pptoas):
+    out, meta = {}, {}
+    archives = {n: nb_archive(pplib, n, *v) for n, v in NB_ARCH.items()}
+    import shutil
+    import tempfile
+    for name, (nchan, nbin, seed, zc) in NB_ARCH.items():
+        model_db = nb_model(pplib, nchan, nbin, 2)  # template channel 2 has weight 0
+
+        def fake_load(filename, **kw):
+            return model_db if filename == "nbmodel.fits" else archives[filename]
+        pptoas.load_data = fake_load
+        pptoas.file_is_type = lambda f, t: (t == "FITS" and f == "nbmodel.fits")
+        gt = quiet_call(pptoas.GetTOAs, name, "nbmodel.fits", quiet=True)
+        quiet_call(gt.get_narrowband_TOAs, quiet=True)
+        lines = []
+        for toa in gt.TOA_list:
+            buf = io.StringIO()
+            with contextlib.redirect_stdout(buf):
+                pplib.write_TOAs(toa, outfile=None)
+            lines.append(buf.getvalue().strip())
+        meta[name] = dict(tim=lines, nchan=nchan, nbin=nbin, seed=seed, zero_chan=zc,
+                          zero_model_chan=2)
+        p = name.split(".")[0] + "_"
+        for attr in ["phis", "phi_errs", "scales", "scale_errs", "channel_snrs",
+                     "channel_red_chi2s"]:
+            out[p + attr] = np.asarray(getattr(gt, attr)[0], dtype=float)
+        out[p + "TOAs"] = np.array([[t.days, t.secs, t.fracsec] if t else [0, 0, 0.0]
+                                    for t in gt.TOAs[0].ravel()])
+        print("narrowband %s: %d TOAs" % (name, len(lines)))
+    MG.save("narrowband.npz", **out)
+    with open(os.path.join(HERE, "narrowband.json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+
+
+# --------------------------------------------------------------------------
+# Channel zapping (pptoas.py:1201-1278 get_channels_to_zap after get_TOAs;
+# ppzap.py:18-48 get_zap_channels): an archive with a spiky channel, a noisy
+# channel and a weak one.
+# --------------------------------------------------------------------------
+ZAP = dict(name="zapA.fits", nsub=3, nchan=32, nbin=512, seed=7007)
+
+
+def zap_archive(pplib):
+    z = ZAP
+    db = synth_archive(pplib, z["name"], z["nsub"], z["nchan"], z["nbin"], z["seed"], 0.0, 0.0)
+    return db
+
+
+def gen_zap(pplib, pptoaslib, pptoas, ppzap):
+    import shutil
+    import tempfile
+    db = zap_archive(pplib)
+    db["subints"] = zap_perturb(db["subints"])
+    db["noise_stds"] = np.array([pplib.get_noise(db["subints"][i, 0], chans=True)
+                                 for i in range(db["nsub"])])[:, None]
+    pptoas.load_data = lambda filename, **kw: db
+    pptoas.file_is_type = lambda f, t: False
+    tmpd = tempfile.mkdtemp()
+    shutil.copy(MG.GMODEL, os.path.join(tmpd, "example.gmodel"))
+    cwd = os.getcwd()
+    os.chdir(tmpd)
+    out = {}
+    try:
+        for tag, kw in [("default", {}), ("snr30", dict(SNR_threshold=30.0, rchi2_threshold=1.2)),
+                        ("noiter", dict(SNR_threshold=30.0, iterate=False))]:
+            gt = quiet_call(pptoas.GetTOAs, ZAP["name"], "example.gmodel", quiet=True)
+            quiet_call(gt.get_TOAs, quiet=True)
+            quiet_call(gt.get_channels_to_zap, **kw)
+            for isub in range(ZAP["nsub"]):
+                out["%s_rchi2_%d" % (tag, isub)] = np.array(gt.channel_red_chi2s[0][isub])
+                out["%s_zap_%d" % (tag, isub)] = np.array(gt.zap_channels[0][isub], dtype=int)
+            print("zap %s: %s" % (tag, gt.zap_channels[0]))
+        for nstd in [3, 1]:
+            zc = ppzap.get_zap_channels(db, nstd=nstd)
+            for isub in range(ZAP["nsub"]):
+                out["median_nstd%d_%d" % (nstd, isub)] = np.array(zc[isub], dtype=int)
+            print("get_zap_channels nstd %d: %s" % (nstd, zc))
+        out["noise_stds"] = db["noise_stds"]
+    finally:
+        os.chdir(cwd)
+    MG.save("zap.npz", **out)
+
+
 def main():
-    what = sys.argv[1:] or ["fit", "configs", "align", "headline", "timing", "tncfloor"]
+    what = sys.argv[1:] or ["fit", "configs", "align", "headline", "timing", "tncfloor",
+                            "narrowband", "zap"]
     np.seterr(all="ignore")
     if "headline" in what:
         gen_headline_2k()
@@ -463,6 +582,11 @@ def main():
             gen_timing(pplib, pptoaslib)
         if "tncfloor" in rest:
             gen_tnc_floor(pplib, pptoaslib)
+        if "narrowband" in rest:
+            gen_narrowband(pplib, pptoaslib, pptoas)
+        if "zap" in rest:
+            import ppzap
+            gen_zap(pplib, pptoaslib, pptoas, ppzap)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 

@@ -171,3 +171,77 @@ def test_headline_2000_subints_vs_reference(gpu):
     np.testing.assert_allclose(r["param_errs"][:, 0], z["phi_err"], rtol=1e-6)
     np.testing.assert_allclose(r["red_chi2"], z["red_chi2"], rtol=1e-9)
     np.testing.assert_allclose(r["snr"], z["snr"], rtol=1e-8)
+
+
+def test_narrowband_toas_vs_reference(gpu):
+    """GetTOAs.get_narrowband_TOAs (pptoas.py:740-1125) with an archive
+    template, against the reference run on the same one-subint archives."""
+    from pulseportraiture_amd import archive, pplib, pptoas, synth
+    meta = json.load(open(os.path.join(GOLDEN, "narrowband.json")))
+    z = np.load(os.path.join(GOLDEN, "narrowband.npz"))
+    for name, m in sorted(meta.items()):
+        nchan, nbin = m["nchan"], m["nbin"]
+        register_synth_archive(name, 1, nchan, nbin, m["seed"], 0.0, 0.0)
+        if m["zero_chan"] is not None:
+            b = dict(archive.load_data(name))
+            b["weights"] = np.array(b["weights"])
+            b["weights"][0, m["zero_chan"]] = 0.0
+            for k in ("ok_ichans", "ok_isubs", "masks"):
+                b.pop(k)
+            archive.register_archive(name, b)
+        w = synth.make_workload(1, nchan, nbin, seed=1)
+        wts = np.ones((1, nchan))
+        wts[0, m["zero_model_chan"]] = 0.0
+        archive.register_archive("nbmodel.fits", dict(subints=w.model[None, None], freqs=w.freqs,
+                                                      Ps=[w.P], epochs=[(57300, 0, 0.0)],
+                                                      weights=wts, DM=DM0))
+        gt = pptoas.GetTOAs([name], "nbmodel.fits", quiet=True)
+        gt.get_narrowband_TOAs(quiet=True)
+        lines = [pplib.toa_line(t) for t in gt.TOA_list]
+        p = name.split(".")[0] + "_"
+        err = z[p + "phi_errs"]
+        fitted = err > 0
+        assert np.array_equal(gt.phi_errs[0] > 0, fitted)
+        assert np.all(np.abs(gt.phis[0] - z[p + "phis"])[fitted] <= 1e-3 * err[fitted])
+        np.testing.assert_allclose(gt.phi_errs[0][fitted], err[fitted], rtol=1e-6)
+        np.testing.assert_allclose(gt.scales[0], z[p + "scales"], rtol=1e-8, atol=1e-12)
+        np.testing.assert_allclose(gt.channel_snrs[0], z[p + "channel_snrs"], rtol=1e-8,
+                                   atol=1e-12)
+        np.testing.assert_allclose(gt.channel_red_chi2s[0], z[p + "channel_red_chi2s"],
+                                   rtol=1e-8)
+        compare_tim(lines, m["tim"])
+
+
+ZAP_CASES = [("default", {}), ("snr30", dict(SNR_threshold=30.0, rchi2_threshold=1.2)),
+             ("noiter", dict(SNR_threshold=30.0, iterate=False))]
+
+
+def test_channels_to_zap_vs_reference(gpu):
+    """GetTOAs.get_channels_to_zap after get_TOAs (pptoas.py:1201-1278) on a
+    3 x 32 x 512 archive with a spiky, a noisy and a dead channel, against
+    the reference's per-channel reduced chi2 and zap lists (zap.npz)."""
+    from pulseportraiture_amd import archive, pptoas, synth
+    from tests.golden_consts import zap_perturb
+    z = np.load(os.path.join(GOLDEN, "zap.npz"))
+    register_synth_archive("zapA.fits", 3, 32, 512, 7007, 0.0, 0.0)
+    b = dict(archive.load_data("zapA.fits"))
+    b["subints"] = zap_perturb(np.asarray(b["subints"]))
+    b["noise_stds"] = z["noise_stds"]
+    for k in ("ok_ichans", "ok_isubs", "masks"):
+        b.pop(k)
+    archive.register_archive("zapA.fits", b)
+    for tag, kw in ZAP_CASES:
+        gt = pptoas.GetTOAs("zapA.fits", synth.EXAMPLE_GMODEL, quiet=True)
+        gt.get_TOAs(quiet=True)
+        gt.get_channels_to_zap(**kw)
+        for isub in range(3):
+            # the fitted phi/DM/scales differ from the reference's by <= 1e-3
+            # sigma, which moves a channel's reduced chi2 by ~1e-7 absolute
+            np.testing.assert_allclose(gt.channel_red_chi2s[0][isub],
+                                       z["%s_rchi2_%d" % (tag, isub)], rtol=1e-5)
+            assert list(gt.zap_channels[0][isub]) == list(z["%s_zap_%d" % (tag, isub)]), tag
+    # show_fit: port and scaled template of subint 1 reproduce the chi2
+    port, model, ok, freqs, noise = gt.show_fit("zapA.fits", isub=1, show=False,
+                                                return_fit=True, quiet=True)
+    rc = [np.sum(((port[c] - model[c]) / noise[c]) ** 2) / (port.shape[1] - 2) for c in ok]
+    np.testing.assert_allclose(rc, z["noiter_rchi2_1"], rtol=1e-5)
