@@ -97,9 +97,12 @@ int ppf_selftest(ppf_ctx* ctx, int32_t* fails);
  * enabled, every k_fit_taylor workgroup adds its wall_clock64 ticks (100 MHz)
  * per phase into device counters: out[0] guess, [1] meta + first moments,
  * [2] centre selection incl. recentring, [3] objective sweeps, [4] trust-
- * region step, [8] recentring passes, [9] workgroups.  The call copies the
+ * region step, [8] recentring passes, [9] workgroups; every k_post
+ * workgroup likewise: [16] meta + Sd, [17] nu_zero sums and solve, [18]
+ * outputs at nu_out + centre pick, [19] with-scales sweep, [20] inverses,
+ * [21] per-channel errors + stores, [22] workgroups.  The call copies the
  * counters to out (if non-null), zeroes them and sets the enable state.   */
-#define PPF_PHASE_N 16
+#define PPF_PHASE_N 32
 int ppf_phase_profile(ppf_ctx* ctx, int32_t enable, uint64_t* out);
 
 /* ---------------------------------------------------------------------- */

@@ -24,7 +24,7 @@ PPF_SOLVE_EXACT = 1
 PPF_SOLVE_EVAL = 2
 PPF_GUESS_DIRECT = 4
 PPF_SELFTEST_N = 10
-PPF_PHASE_N = 16
+PPF_PHASE_N = 32
 
 _dp = ctypes.c_void_p  # device pointers travel as plain addresses
 

@@ -6,6 +6,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -35,6 +36,7 @@ struct ppf_ctx {
   std::string err;
   int64_t ws_limit = (int64_t)32 << 30;
   double2* tw[16] = {nullptr};
+  double2* vp[16] = {nullptr};  // moment power tables (k_vpow)
   Buffer ws;     // per-chunk fit workspace
   Buffer mspec;   // template spectra
   Buffer aux;     // misc (synth templates, partial sums)
@@ -110,6 +112,27 @@ int twiddles(ppf_ctx* ctx, int nbin, const double2** out) {
     HIPCHK(ctx, hipGetLastError());
   }
   *out = ctx->tw[l];
+  return PPF_OK;
+}
+
+int moments_u() {
+  static const int u = [] {
+    const char* e = getenv("PPF_MOMENTS_U");
+    return (e && atoi(e) == 4) ? 4 : 8;
+  }();
+  return u;
+}
+
+int vpow_table(ppf_ctx* ctx, int nbin, const double2** out) {
+  const int l = ilog2_exact(nbin);
+  if (!ctx->vp[l]) {
+    const int rows = kVpowRows(nbin / 2);
+    HIPCHK(ctx, hipMalloc(&ctx->vp[l], (size_t)rows * 16 * sizeof(double2)));
+    hipLaunchKernelGGL(k_vpow, dim3((rows * 16 + 255) / 256), dim3(256), 0, ctx->stream,
+                       ctx->vp[l], nbin / 2, rows);
+    HIPCHK(ctx, hipGetLastError());
+  }
+  *out = ctx->vp[l];
   return PPF_OK;
 }
 
@@ -219,6 +242,8 @@ void ppf_ctx_destroy(ppf_ctx* ctx) {
   for (auto& t : ctx->pending) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
   for (auto e : ctx->pool) (void)hipEventDestroy(e);
   for (auto p : ctx->tw) if (p) (void)hipFree(p);
+  for (auto p : ctx->vp) if (p) (void)hipFree(p);
+  if (ctx->ptime.p) (void)hipFree(ctx->ptime.p);
   if (ctx->ws.p) (void)hipFree(ctx->ws.p);
   if (ctx->mspec.p) (void)hipFree(ctx->mspec.p);
   if (ctx->aux.p) (void)hipFree(ctx->aux.p);
@@ -407,6 +432,9 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   fa.Tcnt = taylor ? reinterpret_cast<int*>(base + offT + cs * 2 * nchan * kMT * sizeof(double2))
                    : nullptr;
   fa.tw = tw;
+  fa.vpow = nullptr;
+  if (taylor)
+    if (int r = vpow_table(ctx, nbin, &fa.vpow)) return r;
   fa.Mmean = Mmean;
   fa.ptime = ctx->phase_prof ? static_cast<unsigned long long*>(ctx->ptime.p) : nullptr;
   fa.o_params = o->params;
@@ -458,9 +486,12 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
       return r;
     if (taylor) {
       if (int r = timed(ctx, PPF_K_MOMENTS, [&] {
-            const dim3 g(nc, (nchan + 8 * kWaves - 1) / (8 * kWaves));
-            // steps in flight: 8 / 16 / 32 time the same (r01 sweep): not load-latency bound
-            hipLaunchKernelGGL(k_moments<16>, g, dim3(kBlock), 0, ctx->stream, fa);
+            const dim3 g(nc, (nchan + 16 * kWaves - 1) / (16 * kWaves));
+            // steps in flight per wave (tuning knob PPF_MOMENTS_U = 4 / 8)
+            if (moments_u() == 4)
+              hipLaunchKernelGGL(k_moments<4>, g, dim3(kBlock), 0, ctx->stream, fa);
+            else
+              hipLaunchKernelGGL(k_moments<8>, g, dim3(kBlock), 0, ctx->stream, fa);
           }))
         return r;
       if (int r = timed(ctx, PPF_K_FIT_TAYLOR, [&] {

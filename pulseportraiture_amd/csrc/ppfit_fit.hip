@@ -537,10 +537,13 @@ __device__ void sweep_taylor0(const FitArgs& a, const Meta& m, const double* prm
 // Each 8-channel group's contributions are reduced across the wave at once
 // and added into the wave's own LDS row, so nothing is carried through the
 // cell loop in registers.
+// lrow (optional, kWaves * 8 rows of LDS): each channel lane (h == 0) adds its
+// terms into its own row across groups and the block sums the rows once at
+// the end, instead of NP wave reductions per channel group.
 template <int MODE, bool SCAT>
 __device__ void sweep(const FitArgs& a, const Meta& m, int c, int s, const double* prm,
                       const double* refs, double P, double* acc_slot, double* out,
-                      double (*red)[48], const TaylorSrc& ts) {
+                      double (*red)[48], const TaylorSrc& ts, double (*lrow)[48] = nullptr) {
   if constexpr (MODE == 0 && !SCAT) {
     if (ts.T && ts.same) {
       sweep_taylor0(a, m, prm, acc_slot, out, red, ts);
@@ -556,6 +559,9 @@ __device__ void sweep(const FitArgs& a, const Meta& m, int c, int s, const doubl
   const int midx = a.model_idx ? a.model_idx[s] : 0;
   constexpr int NP = MODE == 0 ? 21 : 45;
   if (lane < NP) red[w][lane] = 0.0;
+  double* myrow = lrow ? lrow[w * 8 + g8] : nullptr;
+  if (lrow && h == 0)
+    for (int i = 0; i < NP; ++i) myrow[i] = 0.0;
   __syncthreads();
   const int ngroups = (m.nok + 7) >> 3;
   for (int gi = w; gi < ngroups; gi += kWaves) {
@@ -624,16 +630,25 @@ __device__ void sweep(const FitArgs& a, const Meta& m, int c, int s, const doubl
         }
       }
     }
+    if (lrow) {
+      if (h == 0 && valid)
 #pragma unroll
-    for (int i = 0; i < NP; ++i) {
-      const double v = wave_sum(ct[i]);  // only h == 0 lanes hold terms
-      if (lane == 0) red[w][i] += v;
+        for (int i = 0; i < NP; ++i) myrow[i] += ct[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        const double v = wave_sum(ct[i]);  // only h == 0 lanes hold terms
+        if (lane == 0) red[w][i] += v;
+      }
     }
   }
   __syncthreads();
   if (tid < NP) {
     double t = 0.0;
-    for (int q = 0; q < kWaves; ++q) t += red[q][tid];
+    if (lrow)
+      for (int r = 0; r < kWaves * 8; ++r) t += lrow[r][tid];
+    else
+      for (int q = 0; q < kWaves; ++q) t += red[q][tid];
     out[tid] = t;
   }
   __syncthreads();
@@ -964,33 +979,42 @@ __global__ __launch_bounds__(kBlock) void k_solve(FitArgs a) {
 // ---------------------------------------------------------------------------
 // k_post
 // ---------------------------------------------------------------------------
+// The post-fit's serial sections (thread 0) index small arrays at run time;
+// they live in the block's LDS workspace (PostWs), not in per-lane scratch.
+struct PostWs {
+  double c[7], pol[7][7], prev[7], pts[9], cur[7];  // poly_real_roots
+  double roots[7], co[7];                          // closest_positive / nz_solve
+  double M[5][10];                                 // invert_small
+  double A[25], Ci[25];                            // with-scales / no-scales blocks
+};
+
 // Real roots of sum_i c[i] y^(deg-i) (deg <= 6) in ascending order: the roots
 // of the derivative bracket them; each bracket is bisected to convergence.
-__device__ int poly_real_roots(const double* cin, int deg, double* roots) {
-  double c[7];
+__device__ int poly_real_roots(const double* cin, int deg, double* roots, PostWs& w) {
+  double* c = w.c;
   int off = 0;
   while (off <= deg && cin[off] == 0.0) ++off;  // np.roots strips leading zeros
   int d = deg - off;
   for (int i = 0; i <= d; ++i) c[i] = cin[off + i];
   while (d > 0 && c[d] == 0.0) --d;             // trailing zeros: roots at 0 (not > 0)
   if (d <= 0) return 0;
-  double pol[7][7];
+  auto& pol = w.pol;
   for (int i = 0; i <= d; ++i) pol[d][i] = c[i] / c[0];
   for (int o = d - 1; o >= 1; --o)
     for (int i = 0; i <= o; ++i) pol[o][i] = pol[o + 1][i] * (double)(o + 1 - i) / (double)(o + 1);
   double bound = 0.0;
   for (int i = 1; i <= d; ++i) bound = fmax(bound, fabs(pol[d][i]));
   bound = 1.0 + bound;
-  double prev[7];
+  double* prev = w.prev;
   int np_ = 1;
   prev[0] = -pol[1][1];  // linear
   for (int o = 2; o <= d; ++o) {
-    double pts[9];
+    double* pts = w.pts;
     int npts = 0;
     pts[npts++] = -bound;
     for (int i = 0; i < np_; ++i) pts[npts++] = fmin(fmax(prev[i], -bound), bound);
     pts[npts++] = bound;
-    double cur[7];
+    double* cur = w.cur;
     int nc = 0;
     auto ev = [&](double x) {
       double v = pol[o][0];
@@ -1019,8 +1043,8 @@ __device__ int poly_real_roots(const double* cin, int deg, double* roots) {
 }
 
 // Gauss-Jordan inverse with partial pivoting (np.linalg.inv), n <= 5.
-__device__ bool invert_small(const double* A, int n, double* Ai) {
-  double M[5][10];
+__device__ bool invert_small(const double* A, int n, double* Ai, PostWs& w) {
+  auto& M = w.M;
   for (int i = 0; i < n; ++i)
     for (int j = 0; j < 2 * n; ++j) M[i][j] = j < n ? A[i * n + j] : (j - n == i ? 1.0 : 0.0);
   for (int col = 0; col < n; ++col) {
@@ -1044,6 +1068,57 @@ __device__ bool invert_small(const double* A, int n, double* Ai) {
   return true;
 }
 
+// The fitted block of a 5x5 symmetric matrix, inverted in registers: A is
+// padded with the identity on unfitted rows/columns, which Gauss-Jordan with
+// partial pivoting leaves untouched (their pivots are 1, their off-diagonal
+// entries 0 and never chosen as pivots), so the fitted entries of the result
+// are bitwise those of invert_small on the compacted nf x nf block.  Fully
+// unrolled: the pivot row swap is a select over the candidate rows.  Returns
+// false (singular) like invert_small; Ai gets 0 outside the fitted block.
+__device__ __forceinline__ bool invert5_fitted(const double (&A)[5][5], const bool (&fit)[5],
+                                               double (&Ai)[5][5]) {
+  double M[5][10];
+#pragma unroll
+  for (int i = 0; i < 5; ++i)
+#pragma unroll
+    for (int j = 0; j < 10; ++j)
+      M[i][j] = j < 5 ? ((fit[i] && fit[j]) ? A[i][j] : (i == j ? 1.0 : 0.0))
+                      : (j - 5 == i ? 1.0 : 0.0);
+  bool ok = true;
+#pragma unroll
+  for (int col = 0; col < 5; ++col) {
+    int piv = col;
+    double best = fabs(M[col][col]);
+#pragma unroll
+    for (int r = col + 1; r < 5; ++r)
+      if (fabs(M[r][col]) > best) { best = fabs(M[r][col]); piv = r; }
+    if (best == 0.0) ok = false;
+#pragma unroll
+    for (int r = col + 1; r < 5; ++r) {
+      if (piv == r) {
+#pragma unroll
+        for (int j = 0; j < 10; ++j) { const double t = M[col][j]; M[col][j] = M[r][j]; M[r][j] = t; }
+      }
+    }
+    const double iv = 1.0 / M[col][col];
+#pragma unroll
+    for (int j = 0; j < 10; ++j) M[col][j] *= iv;
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      if (r == col) continue;
+      const double fct = M[r][col];
+      if (fct == 0.0) continue;
+#pragma unroll
+      for (int j = 0; j < 10; ++j) M[r][j] -= fct * M[col][j];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 5; ++i)
+#pragma unroll
+    for (int j = 0; j < 5; ++j) Ai[i][j] = (fit[i] && fit[j]) ? M[i][j + 5] : 0.0;
+  return ok;
+}
+
 // Per-channel contributions to the zero-covariance sums (pptoaslib.py:746-901).
 // Returns the number of sums; the branch id is chosen by the caller.
 enum { NZ_NONE = 0, NZ_PD, NZ_PG, NZ_TA, NZ_PDT, NZ_PDG, NZ_PDTA, NZ_PDGT };
@@ -1063,7 +1138,7 @@ __device__ __forceinline__ int nz_branch(const int* ff) {
   }
 }
 
-__device__ void nz_terms(int br, int option, const ChanDeriv& d, double fr, const double* refs,
+__device__ __forceinline__ void nz_terms(int br, int option, const ChanDeriv& d, double fr, const double* refs,
                          const int* fl, double* t) {
   const double f2 = 1.0 / (fr * fr), f4 = f2 * f2, lnf = log(fr);
   auto H = [&](int i, int j) { return (fl[i] && fl[j]) ? Hn_(d, i, j) : 0.0; };
@@ -1132,9 +1207,33 @@ __device__ void nz_terms(int br, int option, const ChanDeriv& d, double fr, cons
   }
 }
 
-__device__ double closest_positive(const double* coeffs, int deg, bool sq, double fmean) {
-  double r[7];
-  const int nr = poly_real_roots(coeffs, deg, r);
+// number of channel sums nz_terms fills for a branch
+__device__ __forceinline__ int nz_nsums(int br) {
+  switch (br) {
+    case NZ_PD: case NZ_PG: case NZ_TA: return 2;
+    case NZ_PDT: return 6;
+    case NZ_PDG: return 8;
+    case NZ_PDGT: return 14;
+    case NZ_PDTA: return 22;
+    default: return 0;
+  }
+}
+
+// block_sum_vec over the first N of 22 sums
+template <int N>
+__device__ __forceinline__ void block_sum_first(double (&v)[22], double (*red)[48]) {
+  double u[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) u[i] = v[i];
+  block_sum_vec(u, red);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = u[i];
+}
+
+__device__ double closest_positive(const double* coeffs, int deg, bool sq, double fmean,
+                                   PostWs& w) {
+  double* r = w.roots;
+  const int nr = poly_real_roots(coeffs, deg, r, w);
   double best = NAN, bd = INFINITY;
   for (int i = 0; i < nr; ++i) {
     if (!(r[i] > 0.0)) continue;
@@ -1146,7 +1245,8 @@ __device__ double closest_positive(const double* coeffs, int deg, bool sq, doubl
 }
 
 // Solve the branch from the channel sums t[22]; writes nz[3] (refs preset).
-__device__ void nz_solve(int br, int option, const double* t, double fmean, double* nz) {
+__device__ void nz_solve(int br, int option, const double* t, double fmean, double* nz,
+                         PostWs& w) {
   switch (br) {
     case NZ_PD: nz[0] = pow(t[0] / t[1], -0.5); break;
     case NZ_PG: nz[1] = pow(t[0] / t[1], -0.25); break;
@@ -1162,8 +1262,12 @@ __device__ void nz_solve(int br, int option, const double* t, double fmean, doub
                      Hh = t[7];
         // coeffs [A C - E G, 0, E H - A D, 0, F G - B C, 0, B D - F H] in nu:
         // a cubic in y = nu^2 (pptoaslib.py:789-794)
-        const double cy[4] = {A * C - E * G, E * Hh - A * D, F * G - B * C, B * D - F * Hh};
-        const double x = closest_positive(cy, 3, true, fmean);
+        double* cy = w.co;
+        cy[0] = A * C - E * G;
+        cy[1] = E * Hh - A * D;
+        cy[2] = F * G - B * C;
+        cy[3] = B * D - F * Hh;
+        const double x = closest_positive(cy, 3, true, fmean, w);
         nz[0] = nz[1] = x;
       }
     } break;
@@ -1182,7 +1286,7 @@ __device__ void nz_solve(int br, int option, const double* t, double fmean, doub
         const double A = t[0], a = t[1], B = t[2], b = t[3], C = t[4], c = t[5], D = t[6],
                      d = t[7], E = t[8], e = t[9], F = t[10], f = t[11], H14 = t[12],
                      H44 = t[13];
-        double co[6];
+        double* co = w.co;
         int deg;
         if (option == 0) {
           co[0] = A * A * B + H44 * C * D + H14 * E * F - H44 * B * E - A * C * F - H14 * A * D;
@@ -1205,7 +1309,7 @@ __device__ void nz_solve(int br, int option, const double* t, double fmean, doub
           co[4] = -a * a * b + a * c * f;
           deg = 4;
         }
-        const double x = closest_positive(co, deg, true, fmean);
+        const double x = closest_positive(co, deg, true, fmean, w);
         nz[0] = nz[1] = x;
       }
     } break;
@@ -1214,6 +1318,8 @@ __device__ void nz_solve(int br, int option, const double* t, double fmean, doub
 }
 
 struct PostShared {
+  PostWs ws;
+  double lrow[kWaves * 8][48];  // with-scales sweep: one row per channel lane
   double prm[5], refs[3], nu[3];
   double out[48];
   double red[kWaves][48];
@@ -1229,6 +1335,16 @@ template <bool SCAT>
 __device__ void post_subint(const FitArgs& a, int c, int s, unsigned char* dyn, PostShared& sh) {
   const int tid = threadIdx.x;
   const int nchan = a.nchan;
+  // diagnostic phase clock (ppf_phase_profile): thread 0 only
+  const bool prof = a.ptime != nullptr;
+  unsigned long long t0 = prof ? wall_clock64() : 0ull;
+  auto mark = [&](int i) {
+    if (prof && tid == 0) {
+      const unsigned long long t1 = wall_clock64();
+      atomicAdd(&a.ptime[i], t1 - t0);
+      t0 = t1;
+    }
+  };
   const Meta m = load_meta(a, c, s, dyn, &sh.nok);
   const SolveState& st = a.st[c];
   const double P = a.P[s];
@@ -1260,6 +1376,7 @@ __device__ void post_subint(const FitArgs& a, int c, int s, unsigned char* dyn, 
     sh.bad = (m.nok == 0);
   }
   __syncthreads();
+  mark(16);
   if (sh.bad) {
     if (tid == 0) {
       for (int i = 0; i < 5; ++i) {
@@ -1297,13 +1414,21 @@ __device__ void post_subint(const FitArgs& a, int c, int s, unsigned char* dyn, 
         for (int i = 0; i < 22; ++i) sums[i] += t[i];
       }
     }
-    block_sum_vec(sums, sh.red);
+    switch (nz_nsums(br)) {  // uniform across the block
+      case 2: block_sum_first<2>(sums, sh.red); break;
+      case 6: block_sum_first<6>(sums, sh.red); break;
+      case 8: block_sum_first<8>(sums, sh.red); break;
+      case 14: block_sum_first<14>(sums, sh.red); break;
+      case 22: block_sum_first<22>(sums, sh.red); break;
+      default: break;
+    }
     if (tid == 0) {
       double nz[3] = {sh.refs[0], sh.refs[1], sh.refs[2]};
-      nz_solve(br, a.option, sums, sh.fmean, nz);
+      nz_solve(br, a.option, sums, sh.fmean, nz, sh.ws);
       for (int i = 0; i < 3; ++i) if (isnan(nuo[i])) nuo[i] = nz[i];
     }
   }
+  mark(17);
   if (tid == 0) {
     if (a.is_toa) {  // pptoaslib.py:1048-1050
       if (a.flags[1]) nuo[1] = nuo[0];
@@ -1348,40 +1473,53 @@ __device__ void post_subint(const FitArgs& a, int c, int s, unsigned char* dyn, 
     ts = TaylorSrc{a.T + ((size_t)c * 2 + best) * nchan * kMT,
                    a.Tcnt + ((size_t)c * 2 + best) * nchan, st.xc[best], st.refs};
   }
-  sweep<1, SCAT>(a, m, c, s, sh.prm, sh.nu, P, nullptr, sh.out, sh.red, ts);
+  mark(18);
+  sweep<1, SCAT>(a, m, c, s, sh.prm, sh.nu, P, nullptr, sh.out, sh.red, ts, sh.lrow);
+  mark(19);
   if (tid == 0) {
-    const int nf = sh.nfit;
-    double A[25];
-    #pragma unroll
+    bool fit[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) fit[i] = a.flags[i] != 0;
+    double A[5][5], Ai[5][5];
+#pragma unroll
     for (int p = 0; p < 15; ++p) {
       const int pi = pair_i(p), pj = pair_j(p);
-      int ii = -1, jj = -1;
-      for (int q = 0; q < nf; ++q) { if (sh.ifit[q] == pi) ii = q; if (sh.ifit[q] == pj) jj = q; }
-      if (ii < 0 || jj < 0) continue;
-      const double v = sh.out[p] - sh.out[15 + p];  // A - U C^-1 V
-      A[ii * nf + jj] = v;
-      A[jj * nf + ii] = v;
+      A[pi][pj] = A[pj][pi] = sh.out[p] - sh.out[15 + p];  // A - U C^-1 V
     }
-    if (!invert_small(A, nf, sh.Xinv))
-      for (int i = 0; i < nf * nf; ++i) sh.Xinv[i] = NAN;
+    const bool ok = invert5_fitted(A, fit, Ai);
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+      for (int j = 0; j < 5; ++j)
+        sh.Xinv[i * 5 + j] = ok ? Ai[i][j] : ((fit[i] && fit[j]) ? NAN : 0.0);
     if (a.o_cov_nosc) {
+#pragma unroll
       for (int p = 0; p < 15; ++p) {
         const int pi = pair_i(p), pj = pair_j(p);
-        int ii = -1, jj = -1;
-        for (int q = 0; q < nf; ++q) { if (sh.ifit[q] == pi) ii = q; if (sh.ifit[q] == pj) jj = q; }
-        if (ii < 0 || jj < 0) continue;
-        A[ii * nf + jj] = A[jj * nf + ii] = 0.5 * sh.out[30 + p];
+        A[pi][pj] = A[pj][pi] = 0.5 * sh.out[30 + p];
       }
-      double Ci[25];
-      if (!invert_small(A, nf, Ci))
-        for (int i = 0; i < nf * nf; ++i) Ci[i] = NAN;
+      const bool okc = invert5_fitted(A, fit, Ai);
       double* cn = a.o_cov_nosc + (size_t)s * 25;
+      // compacted to the fitted block's leading nf x nf corner (as before)
+      int q = 0;
+#pragma unroll
       for (int i = 0; i < 25; ++i) cn[i] = 0.0;
-      for (int q = 0; q < nf; ++q)
-        for (int r = 0; r < nf; ++r) cn[q * 5 + r] = Ci[q * nf + r];
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        if (!fit[i]) continue;
+        int r = 0;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+          if (!fit[j]) continue;
+          cn[q * 5 + r] = okc ? Ai[i][j] : NAN;
+          ++r;
+        }
+        ++q;
+      }
     }
   }
   __syncthreads();
+  mark(20);
   // ---- per-channel amplitude errors and S/N (pptoaslib.py:717-724, 1079-1082) ----
   const int nf = sh.nfit;
   double snr2 = 0.0;
@@ -1389,20 +1527,23 @@ __device__ void post_subint(const FitArgs& a, int c, int s, unsigned char* dyn, 
     const double* w = a.wsc + ((size_t)c * nchan + j) * 8;
     const double sc = w[0], S = w[1];
     const double ic = 1.0 / (2.0 * S);
+    // fitted parameters in order; Xinv is 0 outside the fitted block, and
+    // adding its zeros leaves the compact sums bitwise unchanged
     double LL[5], U[5];
 #pragma unroll
-    for (int q = 0; q < 5; ++q) U[q] = q < nf ? w[2 + sh.ifit[q]] : 0.0;
+    for (int q = 0; q < 5; ++q) U[q] = a.flags[q] ? w[2 + q] : 0.0;
 #pragma unroll
     for (int q = 0; q < 5; ++q) {
       double t = 0.0;
 #pragma unroll
       for (int i = 0; i < 5; ++i)
-        if (i < nf && q < nf) t += U[i] * sh.Xinv[i * nf + q];
+        if (a.flags[i] && a.flags[q]) t += U[i] * sh.Xinv[i * 5 + q];
       LL[q] = -ic * t;
     }
     double t = 0.0;
 #pragma unroll
-    for (int q = 0; q < 5; ++q) t += LL[q] * U[q];
+    for (int q = 0; q < 5; ++q)
+      if (a.flags[q]) t += LL[q] * U[q];
     const double LR = -t * ic + ic;
     const double csnr = sc * sqrt(S);
     const int n = m.chan[j];
@@ -1419,9 +1560,17 @@ __device__ void post_subint(const FitArgs& a, int c, int s, unsigned char* dyn, 
     for (int i = 0; i < 5; ++i) { op[i] = sh.prm[i]; oe[i] = 0.0; }
     double* cv = a.o_cov + (size_t)s * 25;
     for (int i = 0; i < 25; ++i) cv[i] = 0.0;
-    for (int q = 0; q < nf; ++q) {
-      oe[sh.ifit[q]] = sqrt(2.0 * sh.Xinv[q * nf + q]);
-      for (int r = 0; r < nf; ++r) cv[q * 5 + r] = 2.0 * sh.Xinv[q * nf + r];
+    int q = 0;
+    for (int i = 0; i < 5; ++i) {
+      if (!a.flags[i]) continue;
+      oe[i] = sqrt(2.0 * sh.Xinv[i * 5 + i]);
+      int r = 0;
+      for (int j = 0; j < 5; ++j) {
+        if (!a.flags[j]) continue;
+        cv[q * 5 + r] = 2.0 * sh.Xinv[i * 5 + j];
+        ++r;
+      }
+      ++q;
     }
     for (int i = 0; i < 3; ++i) a.o_nu_out[(size_t)s * 3 + i] = sh.nu[i];
     const double dof = (double)a.nbin * (double)m.nok - (double)(nf + m.nok);
@@ -1434,13 +1583,15 @@ __device__ void post_subint(const FitArgs& a, int c, int s, unsigned char* dyn, 
     if (a.o_init_used) for (int i = 0; i < 5; ++i) a.o_init_used[(size_t)s * 5 + i] = st.init[i];
     if (a.o_fun) a.o_fun[s] = st.fun;
   }
+  mark(21);
+  if (prof && tid == 0) atomicAdd(&a.ptime[22], 1ull);
 }
 
 // Phase-family post-fit: capped at 128 VGPRs for four waves per SIMD (its
 // serial thread-0 sections are latency-bound; 1.16 -> 1.00 ms at config 2
 // despite the spills).  The scattering variant keeps its registers.
 template <bool SCAT>
-__global__ __launch_bounds__(kBlock, SCAT ? 1 : 4) void k_post(FitArgs a) {
+__global__ __launch_bounds__(kBlock, SCAT ? 1 : 2) void k_post(FitArgs a) {
   extern __shared__ __align__(16) unsigned char dyn[];
   __shared__ PostShared sh;
   const int c = blockIdx.x, s = a.sub0 + c;

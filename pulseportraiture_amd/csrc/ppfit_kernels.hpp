@@ -45,6 +45,9 @@ struct PhaseShiftArgs {
 // is accepted while |y| <= kTaylorY, where the truncation
 // kTaylorY^kMTerm / kMTerm! e^kTaylorY is < 2e-17 of sum_k |W_k|.
 constexpr int kMT = 32;
+// rows of the moment power table: every harmonic a moment block can touch
+// (k <= N plus the zero-padded tail of the last block of steps)
+__host__ __device__ constexpr int kVpowRows(int N) { return N + 1 + 4 * 64; }
 constexpr int kMTerm = kMT - 2;
 constexpr double kTaylorY = 3.0;
 
@@ -88,6 +91,7 @@ struct FitArgs {
   double2* T;                // chunk [c][2][nchan][kMT] Taylor moments
   int* Tcnt;                 // chunk [c][2][nchan] moments stored per row
   const double2* tw;         // rfft twiddles e^{-2 pi i m / nbin}
+  const double2* vpow;       // [kVpowRows(N)][16] (v^col, v^(16+col)), v = k / N
   const double2* Mmean;      // [nmodel][NHP] mean template spectrum or null
   unsigned long long* ptime; // [PPF_PHASE_N] k_fit_taylor phase clocks, or null
   double* acc;               // chunk [c][2][nchan][10]
@@ -403,6 +407,7 @@ __global__ void k_rot_accum(const double* data, const double* phase, const doubl
                             const double2* tw);
 __global__ void k_accum_reduce(const double2* partial, double2* accum, int nsplit, size_t count);
 template <int LOGN> __global__ void k_resid_chi2(ResidArgs a, const double2* tw);
+__global__ void k_vpow(double2* vp, int N, int rows);
 __global__ void k_guess(FitArgs a);
 __global__ void k_model_mean(const double2* M, double2* Mmean, int nchan, int NHP);
 __global__ void k_fit_taylor(FitArgs a);

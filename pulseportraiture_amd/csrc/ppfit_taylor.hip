@@ -65,40 +65,141 @@ __device__ __forceinline__ void rs_swap(const double* v, double* out) {
 // Moments of the fitted channels of subint c about centre xc (at refs), from
 // the cross-spectrum rows X written by k_data_xspec, into T[c][slot]:
 //   T_nm = sum_k v_k^m W_nk,  v_k = k / N,  W_nk = X_nk e^{2 pi i k phi_c,n}.
-// The k-contraction runs on the f64 matrix cores: each wave takes tiles of 8
+// The k-contraction runs on the f64 matrix cores: each wave takes tiles of 16
 // fitted channels; per step of 4 harmonics, v_mfma_f64_16x16x4 multiplies
-// A = v^m (16 moments x 4 harmonics) by B = W (4 harmonics x 16 columns =
-// 8 channels x re/im) into two accumulators (moments 0-15, 16-31).  Lane l
-// supplies harmonic 4 s + (l >> 4) of channel (l & 15) >> 1, part l & 1 to B
-// and v^(l & 15), v^(16 + (l & 15)) of that harmonic to A (by squaring; v is
-// exact since N is a power of two).  X rows stream through registers kMomU
-// steps ahead of the MFMAs, so every wave keeps kMomU row loads in flight and
-// the pass runs at HBM rate instead of load latency.  All kMT moments are
+// A = v^m (16 moments x 4 harmonics) by B = Re W and by B = Im W (4 harmonics
+// x 16 channels) into accumulators for moments 0-15 and 16-31.  Lane l
+// supplies harmonic 4 s + (l >> 4) of channel l & 15 to B and v^(l & 15),
+// v^(16 + (l & 15)) of that harmonic to A (v is exact since N is a power of
+// two).  X rows stream through registers U steps ahead of the MFMAs.  All kMT moments are
 // kept (cnt = kMT): the truncation bound then holds for any spectrum.
 // ---------------------------------------------------------------------------
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
-// One 8-channel tile by one wave: lane l handles channel n (of column
-// (l & 15) >> 1; ok = fitted) with centre phase phic; U = steps in flight.
-// Steps go in pairs (u, u + 1): lane part p loads X at the harmonic of step
-// u + p, so the 8 lanes of a channel read one whole 128-B line per pair and
-// no element is fetched twice; each lane rotates its own element, keeps the
-// part it needs and trades the other with its partner (DPP quad_perm
-// [1,0,3,2]): partner lanes differ only in p.
+// v^col and v^(16+col) of harmonic k (v = k iN), in the table's fixed order.
+__device__ __forceinline__ double2 vpow_inline(int k, double iN, int col) {
+  const double v = (double)k * iN;
+  const double v2 = v * v, v4 = v2 * v2, v8 = v4 * v4;
+  double pc = (col & 1) ? v : 1.0;
+  pc *= (col & 2) ? v2 : 1.0;
+  pc *= (col & 4) ? v4 : 1.0;
+  pc *= (col & 8) ? v8 : 1.0;
+  return cmk(pc, pc * (v8 * v8));
+}
+
+// The A operand, v^m for the harmonic k = 4 step + (l >> 4) of a lane and
+// its moment rows m = l & 15 and 16 + (l & 15), comes from a table built once
+// per nbin (k_vpow): the powers are the same for every channel, so forming
+// them per step (3 squarings, 4 selected products and 2 more for v^16+m, on
+// every lane) would cost more vector issue than the two MFMAs they feed.
+// Entries are formed in one fixed order: v, v^2, v^4, v^8 by squaring, the
+// factors of m multiplied in bit order, v^(16+m) = v^m (v^8 v^8).
+__global__ void k_vpow(double2* vp, int N, int rows) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * 16) return;
+  const int k = i >> 4, col = i & 15;
+  vp[i] = vpow_inline(k, 1.0 / (double)N, col);
+}
+
+// One 16-channel tile by one wave: lane l handles channel n (column l & 15 of
+// the B operand; ok = fitted) at harmonic offset l >> 4, with centre phase
+// phic; U = steps in flight.  Each step is four MFMAs: re and im parts of W
+// (two B matrices, 16 channels each) times the moment rows 0-15 and 16-31 of
+// A, with even and odd steps in separate accumulators (independent chains).
+// A lane rotates its own element and feeds it straight to the matrix core:
+// no cross-lane trade, no select.  Its two phasor chains (even / odd steps)
+// restart from turn_phasor every block.  The next block's X and power rows
+// stream into each step's registers as soon as its MFMAs have issued, so U
+// steps of loads stay in flight with one register set.
 template <int U>
-__device__ __forceinline__ void moment_tile(const FitArgs& a, int c, int slot, int n, bool ok,
-                                            double phic) {
+__device__ __forceinline__ void moment_tile16(const FitArgs& a, int c, int slot, int n, bool ok,
+                                              double phic) {
   static_assert(kMT == 32, "two 16-row MFMA tiles");
   static_assert(U % 2 == 0, "steps go in pairs");
   constexpr int UP = U / 2;
   const int lane = threadIdx.x & 63;
   const int N = a.nbin / 2;
-  const double iN = 1.0 / (double)N;
   const int nblk = ((N + 1 + 3) / 4 + U - 1) / U;  // blocks of U 4-harmonic steps
+  const int col = lane & 15, kk = lane >> 4;
+  const double2* __restrict__ Xr = a.X + ((size_t)c * a.nchan + (ok ? n : 0)) * a.NHP;
+  // power row of step t for this lane: vpow[(4 t + kk) * 16 + col]
+  const double2* __restrict__ vp = a.vpow + (size_t)kk * 16 + col;
+  const double2 s8 = turn_phasor(8.0, phic);
+  // re (d) and im (g) parts; moments 0-15 / 16-31; even / odd steps
+  f64x4 d0 = {0.0, 0.0, 0.0, 0.0}, d1 = d0, d2 = d0, d3 = d0;
+  f64x4 g0 = d0, g1 = d0, g2 = d0, g3 = d0;
+  double2 xb[U], pb[U];
+#pragma unroll
+  for (int t = 0; t < U; ++t) {
+    const int k = 4 * t + kk;
+    xb[t] = (ok && k <= N) ? Xr[k] : cmk(0.0, 0.0);
+    pb[t] = vp[(size_t)t * 64];
+  }
+  for (int b = 0; b < nblk; ++b) {
+    const bool more = b + 1 < nblk;
+    double2 e0 = turn_phasor((double)(4 * (b * U) + kk), phic);
+    double2 e1 = turn_phasor((double)(4 * (b * U + 1) + kk), phic);
+#pragma unroll
+    for (int u = 0; u < UP; ++u) {
+      const double2 W0 = cmul(xb[2 * u], e0), W1 = cmul(xb[2 * u + 1], e1);
+      const double2 p0 = pb[2 * u], p1 = pb[2 * u + 1];
+      d0 = __builtin_amdgcn_mfma_f64_16x16x4f64(p0.x, W0.x, d0, 0, 0, 0);
+      d1 = __builtin_amdgcn_mfma_f64_16x16x4f64(p0.y, W0.x, d1, 0, 0, 0);
+      g0 = __builtin_amdgcn_mfma_f64_16x16x4f64(p0.x, W0.y, g0, 0, 0, 0);
+      g1 = __builtin_amdgcn_mfma_f64_16x16x4f64(p0.y, W0.y, g1, 0, 0, 0);
+      d2 = __builtin_amdgcn_mfma_f64_16x16x4f64(p1.x, W1.x, d2, 0, 0, 0);
+      d3 = __builtin_amdgcn_mfma_f64_16x16x4f64(p1.y, W1.x, d3, 0, 0, 0);
+      g2 = __builtin_amdgcn_mfma_f64_16x16x4f64(p1.x, W1.y, g2, 0, 0, 0);
+      g3 = __builtin_amdgcn_mfma_f64_16x16x4f64(p1.y, W1.y, g3, 0, 0, 0);
+      e0 = cmul(e0, s8);
+      e1 = cmul(e1, s8);
+      // rolling prefetch: this pair's registers take the next block's rows
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int t = 2 * u + h;
+        const int k = 4 * ((b + 1) * U + t) + kk;
+        xb[t] = (more && ok && k <= N) ? Xr[k] : cmk(0.0, 0.0);
+        if (more) pb[t] = vp[(size_t)((b + 1) * U + t) * 64];
+      }
+    }
+  }
+  d0 += d2;
+  d1 += d3;
+  g0 += g2;
+  g1 += g3;
+  // D[row = moment (l >> 4) + 4 r][col = channel l & 15]
+  if (ok) {
+    double2* Tn = a.T + (((size_t)c * 2 + slot) * a.nchan + n) * kMT;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      Tn[kk + 4 * r] = cmk(d0[r], g0[r]);
+      Tn[16 + kk + 4 * r] = cmk(d1[r], g1[r]);
+    }
+    if (kk == 0) a.Tcnt[((size_t)c * 2 + slot) * a.nchan + n] = kMT;
+  }
+}
+
+// The same moments from an 8-channel tile (recentring inside k_fit_taylor,
+// whose registers leave room for four accumulators only): lane l holds
+// channel (l & 15) >> 1, part p = l & 1; steps go in pairs, lane part p
+// loads X at the harmonic of step 2u + p and rotates it on its own phasor
+// chain (the p chain of moment_tile16), keeps the part it feeds to B and
+// trades the other with its partner (DPP quad_perm [1,0,3,2]).  Powers are
+// formed inline in the table's order, and every MFMA sees the operands of
+// moment_tile16: bitwise the same moments.
+template <int U>
+__device__ __forceinline__ void moment_tile8(const FitArgs& a, int c, int slot, int n, bool ok,
+                                             double phic) {
+  static_assert(kMT == 32, "two 16-row MFMA tiles");
+  static_assert(U % 2 == 0, "steps go in pairs");
+  constexpr int UP = U / 2;
+  const int lane = threadIdx.x & 63;
+  const int N = a.nbin / 2;
+  const int nblk = ((N + 1 + 3) / 4 + U - 1) / U;
   const int col = lane & 15, part = col & 1, kk = lane >> 4;
   const double2* __restrict__ Xr = a.X + ((size_t)c * a.nchan + (ok ? n : 0)) * a.NHP;
   const double2 s8 = turn_phasor(8.0, phic);
-  // two accumulator pairs (even / odd steps): independent MFMA chains
+  const double iN = 1.0 / (double)N;
   f64x4 d0 = {0.0, 0.0, 0.0, 0.0}, d1 = d0, d2 = d0, d3 = d0;
   double2 xb[UP];
 #pragma unroll
@@ -107,13 +208,7 @@ __device__ __forceinline__ void moment_tile(const FitArgs& a, int c, int slot, i
     xb[u] = (ok && k <= N) ? Xr[k] : cmk(0.0, 0.0);
   }
   for (int b = 0; b < nblk; ++b) {
-    double2 xn[UP];
     const bool more = b + 1 < nblk;
-#pragma unroll
-    for (int u = 0; u < UP; ++u) {
-      const int k = 4 * ((b + 1) * U + 2 * u + part) + kk;
-      xn[u] = (more && ok && k <= N) ? Xr[k] : cmk(0.0, 0.0);
-    }
     double2 e = turn_phasor((double)(4 * (b * U + part) + kk), phic);
 #pragma unroll
     for (int u = 0; u < UP; ++u) {
@@ -121,28 +216,16 @@ __device__ __forceinline__ void moment_tile(const FitArgs& a, int c, int slot, i
       const double recv = dpp_mov<0xB1>(part ? W.x : W.y);
       const double bv0 = part ? recv : W.x;  // step 2u: part p of the even harmonic
       const double bv1 = part ? W.y : recv;  // step 2u + 1
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const double v = (double)(4 * (b * U + 2 * u + h) + kk) * iN;
-        const double v2 = v * v, v4 = v2 * v2, v8 = v4 * v4;
-        double pc = (col & 1) ? v : 1.0;
-        pc *= (col & 2) ? v2 : 1.0;
-        pc *= (col & 4) ? v4 : 1.0;
-        pc *= (col & 8) ? v8 : 1.0;
-        const double pc16 = pc * (v8 * v8);
-        const double bv = h ? bv1 : bv0;
-        if (h) {
-          d2 = __builtin_amdgcn_mfma_f64_16x16x4f64(pc, bv, d2, 0, 0, 0);
-          d3 = __builtin_amdgcn_mfma_f64_16x16x4f64(pc16, bv, d3, 0, 0, 0);
-        } else {
-          d0 = __builtin_amdgcn_mfma_f64_16x16x4f64(pc, bv, d0, 0, 0, 0);
-          d1 = __builtin_amdgcn_mfma_f64_16x16x4f64(pc16, bv, d1, 0, 0, 0);
-        }
-      }
+      const double2 p0 = vpow_inline(4 * (b * U + 2 * u) + kk, iN, col);
+      const double2 p1 = vpow_inline(4 * (b * U + 2 * u + 1) + kk, iN, col);
+      d0 = __builtin_amdgcn_mfma_f64_16x16x4f64(p0.x, bv0, d0, 0, 0, 0);
+      d1 = __builtin_amdgcn_mfma_f64_16x16x4f64(p0.y, bv0, d1, 0, 0, 0);
+      d2 = __builtin_amdgcn_mfma_f64_16x16x4f64(p1.x, bv1, d2, 0, 0, 0);
+      d3 = __builtin_amdgcn_mfma_f64_16x16x4f64(p1.y, bv1, d3, 0, 0, 0);
       e = cmul(e, s8);
+      const int k = 4 * ((b + 1) * U + 2 * u + part) + kk;
+      xb[u] = (more && ok && k <= N) ? Xr[k] : cmk(0.0, 0.0);
     }
-#pragma unroll
-    for (int u = 0; u < UP; ++u) xb[u] = xn[u];
   }
   d0 += d2;
   d1 += d3;
@@ -166,15 +249,15 @@ __device__ void moments_from_X(const FitArgs& a, const Meta& m, int c, int s, in
   for (int t = w; t * 8 < m.nok; t += kWaves) {
     const int j = t * 8 + chl;
     const bool ok = j < m.nok;
-    moment_tile<8>(a, c, slot, ok ? m.chan[j] : 0, ok,
-                   ok ? phase_frac(xc, m.fr[j], refs, P) : 0.0);
+    moment_tile8<8>(a, c, slot, ok ? m.chan[j] : 0, ok,
+                    ok ? phase_frac(xc, m.fr[j], refs, P) : 0.0);
   }
 }
 
 // ---------------------------------------------------------------------------
 // k_moments: the first moment pass of every phase-family subint, about its
 // start point st.xc[0] (k_guess), into T slot 0 -- a pure stream over X at
-// full occupancy.  Block (c, y): wave w takes channels 8 (4 y + w) .. + 7
+// full occupancy.  Block (c, y): wave w takes channels 16 (4 y + w) .. + 15
 // (masked channels idle in their lane).
 // ---------------------------------------------------------------------------
 template <int U>
@@ -182,17 +265,18 @@ __global__ __launch_bounds__(kBlock) void k_moments(FitArgs a) {
   const int c = blockIdx.x, s = a.sub0 + c;
   if (!fused_taylor(a, s)) return;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int n0 = 8 * (kWaves * (int)blockIdx.y + w);
+  const int n0 = 16 * (kWaves * (int)blockIdx.y + w);
   if (n0 >= a.nchan) return;  // whole wave
   const SolveState& st = a.st[c];
-  const int n = n0 + ((lane & 15) >> 1);
+  const int n = n0 + (lane & 15);
   const bool ok = n < a.nchan && (!a.mask || a.mask[(size_t)s * a.nchan + n]);
   const double phic = ok ? phase_frac(st.xc[0], a.freqs[(size_t)s * a.nchan + n], st.refs, a.P[s])
                          : 0.0;
-  moment_tile<U>(a, c, 0, n, ok, phic);
+  moment_tile16<U>(a, c, 0, n, ok, phic);
 }
 
-template __global__ void k_moments<16>(FitArgs);
+template __global__ void k_moments<4>(FitArgs);
+template __global__ void k_moments<8>(FitArgs);
 
 // ---------------------------------------------------------------------------
 // k_fit_taylor: one workgroup per phase-family subint, the whole fit:

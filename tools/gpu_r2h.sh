@@ -1,0 +1,13 @@
+#!/bin/bash
+# round-2 GPU pass h: full GPU suite + headline bench after the post/moments changes
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R" || exit 1
+mkdir -p gpurun_out
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r2h_tests.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/r2h_tests.log; exit 1; }
+tail -2 gpurun_out/r2h_tests.log
+timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --cpu-sample 0 > gpurun_out/r2h_bench.log 2>&1 || { echo "bench failed"; tail -5 gpurun_out/r2h_bench.log; exit 1; }
+python - <<'PY'
+import json
+d = json.loads(open("gpurun_out/r2h_bench.log").read().strip().splitlines()[-1])
+print(d["ms_per_step"], d["roofline"]["kernel_ms_per_step"], d.get("parity_sample"))
+PY
