@@ -101,7 +101,7 @@ def load_library(path=None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    p = path or os.environ.get("PPF_LIB") or LIB_PATH
     if not os.path.exists(p):
         raise RuntimeError(
             "libppfit.so not found at %s: build it with "

@@ -4,6 +4,13 @@
 // and the LDS-resident Stockham FFT used for every real<->complex transform
 // on the hot path (numpy.fft.rfft / irfft in the reference: pplib.py:27).
 #pragma once
+
+#ifndef PPF_NT
+// streaming (non-temporal) hints on the data pass's read-once portrait rows
+// and write-once cross-spectrum rows: 5.57 -> 5.04 ms at config 2 (r02; the
+// moment pass's X loads were slower with the hint and stay plain)
+#define PPF_NT 1
+#endif
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <type_traits>
@@ -477,6 +484,27 @@ __device__ __forceinline__ double2 irfft_pre(double2 xk, double2 xnk, int k, con
 
 namespace ppf {
 
+// Read-once / write-once rows: non-temporal when PPF_NT (streaming hint).
+typedef double f64x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ double2 ld_stream(const double2* p) {
+#if PPF_NT
+  const f64x2v v = __builtin_nontemporal_load(reinterpret_cast<const f64x2v*>(p));
+  return cmk(v.x, v.y);
+#else
+  return *p;
+#endif
+}
+__device__ __forceinline__ void st_stream(double2 v, double2* p) {
+#if PPF_NT
+  f64x2v w;
+  w.x = v.x;
+  w.y = v.y;
+  __builtin_nontemporal_store(w, reinterpret_cast<f64x2v*>(p));
+#else
+  *p = v;
+#endif
+}
+
 // ---------------------------------------------------------------------------
 // Wave-per-row streaming (k_data_xspec, k_moments): each wave owns one LDS
 // row buffer of N + 8 packed complex slots and walks its own channel list,
@@ -498,7 +526,7 @@ struct WaveRow {
       for (int i = 0; i < LI; ++i) {
         const int j = lane + 64 * i;
         if (N >= 64 || j < N) {
-          const double2 v = r2[j];
+          const double2 v = ld_stream(r2 + j);  // read once
           x[i] = v.x;
           y[i] = v.y;
         }
@@ -642,14 +670,17 @@ __device__ __forceinline__ void fft1024_wave(const double (&x)[16], const double
   fft_sync<true>();
   const bool p = (lane & 2) != 0, q = (lane & 1) != 0;
   const int u = (p ? 1 : 0) + (q ? 2 : 0);
+  // radix-2 steps as fma(+-1, own, partner): o - a on the upper lane, a + o on
+  // the lower one, each rounded once exactly as the add / sub it replaces
+  const double sp = p ? -1.0 : 1.0, sq = q ? -1.0 : 1.0;
 #pragma unroll
   for (int s = 0; s < 16; ++s) {
     const double2 a = s ? cmul(v[dft16_pos(s)], tw_pow(s, lo, hi)) : v[0];
     const double2 o = cmk(dpp_mov<0x4E>(a.x), dpp_mov<0x4E>(a.y));  // lane ^ 2
-    double2 b = p ? csub(o, a) : cadd(a, o);
+    double2 b = cmk(fma(sp, a.x, o.x), fma(sp, a.y, o.y));
     if (p && q) b = mul_negi(b);
     const double2 o2 = cmk(dpp_mov<0xB1>(b.x), dpp_mov<0xB1>(b.y));  // lane ^ 1
-    buf[rr + 16 * s + 260 * u] = q ? csub(o2, b) : cadd(b, o2);
+    buf[rr + 16 * s + 260 * u] = cmk(fma(sq, b.x, o2.x), fma(sq, b.y, o2.y));
   }
   fft_sync<true>();
 }

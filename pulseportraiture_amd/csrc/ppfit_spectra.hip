@@ -238,8 +238,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
           if (k >= 1) pd += p2k;
           if (two) pd += p2n;
           if (wx) {
-            Xr[k] = (k == 0) ? cmk(0.0, 0.0) : cmulc(xk, mk);
-            if (two) Xr[kn] = cmulc(xn, mn);
+            st_stream((k == 0) ? cmk(0.0, 0.0) : cmulc(xk, mk), Xr + k);
+            if (two) st_stream(cmulc(xn, mn), Xr + kn);
           }
           if (a.guess) {
             // e^{2 pi i (N-k) phi} = e^{2 pi i N phi} conj(e^{2 pi i k phi});

@@ -76,6 +76,9 @@ __device__ __forceinline__ void rs_swap(const double* v, double* out) {
 // ---------------------------------------------------------------------------
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
+// X rows: plain loads (the non-temporal hint measured slower here)
+__device__ __forceinline__ double2 xload(const double2* p) { return *p; }
+
 // v^col and v^(16+col) of harmonic k (v = k iN), in the table's fixed order.
 __device__ __forceinline__ double2 vpow_inline(int k, double iN, int col) {
   const double v = (double)k * iN;
@@ -132,7 +135,7 @@ __device__ __forceinline__ void moment_tile16(const FitArgs& a, int c, int slot,
 #pragma unroll
   for (int t = 0; t < U; ++t) {
     const int k = 4 * t + kk;
-    xb[t] = (ok && k <= N) ? Xr[k] : cmk(0.0, 0.0);
+    xb[t] = (ok && k <= N) ? xload(Xr + k) : cmk(0.0, 0.0);
     pb[t] = vp[(size_t)t * 64];
   }
   for (int b = 0; b < nblk; ++b) {
@@ -158,7 +161,7 @@ __device__ __forceinline__ void moment_tile16(const FitArgs& a, int c, int slot,
       for (int h = 0; h < 2; ++h) {
         const int t = 2 * u + h;
         const int k = 4 * ((b + 1) * U + t) + kk;
-        xb[t] = (more && ok && k <= N) ? Xr[k] : cmk(0.0, 0.0);
+        xb[t] = (more && ok && k <= N) ? xload(Xr + k) : cmk(0.0, 0.0);
         if (more) pb[t] = vp[(size_t)((b + 1) * U + t) * 64];
       }
     }
