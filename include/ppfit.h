@@ -18,6 +18,8 @@
  *                              ppalign.py:202-208
  *   ppf_irfft_rows          <- numpy.fft.irfft (final step of ppalign.py:210-213)
  *   ppf_noise_rows          <- pplib.get_noise_PS(chans=True)  pplib.py:2227-2253
+ *   ppf_gaussian_portraits  <- pplib.gen_gaussian_portrait / read_model
+ *                              pplib.py:853-930, 2873-2959
  *   ppf_scatter_rotate_rows <- GetTOAs.show_fit port/model  pptoas.py:1389-1402
  *   ppf_resid_chi2_rows     <- pplib.get_red_chi2 per channel in
  *                              GetTOAs.get_channels_to_zap  pptoas.py:1201-1278
@@ -205,6 +207,18 @@ int ppf_rotate_rows(ppf_ctx* ctx, int32_t nrow, int32_t nbin, const double* in,
 int ppf_rotate_accumulate(ppf_ctx* ctx, int32_t nsub, int32_t nchan,
                           int32_t nbin, const double* data, const double* phase,
                           const double* weight, double* accum);
+
+/* Gaussian-component template rows (gen_gaussian_portrait, pplib.py:853-930,
+ * as read_model calls it, pplib.py:2873-2959): out[r][:] at freqs[r] for
+ * nrow rows (portraits x channels, any mix of frequencies).  code: HOST
+ * int32[3], the evolution of loc / wid / amp (0 power law, 1 linear:
+ * evolve_parameter, pplib.py:1030-1046); params: HOST double[2 + 6 ngauss],
+ * DC, TAU [bin] (read_model's TAU * nbin / P), then per component loc,
+ * dloc, wid, dwid, amp, damp; ngauss <= 32.  TAU != 0 scatters row r by
+ * TAU / nbin (freqs[r] / nu_ref)^alpha.  out may not alias freqs.        */
+int ppf_gaussian_portraits(ppf_ctx* ctx, int32_t nrow, int32_t nbin, int32_t ngauss,
+                           const int32_t* code, const double* params, double nu_ref,
+                           double alpha, const double* freqs, double* out);
 
 /* out[r] = irfft(rfft(in[r]) e^{2 pi i k phase[r]} / (1 + 2 pi i k tau[r]))
  * (rotate_portrait_full of a scattered template, pptoas.py:1389-1397);

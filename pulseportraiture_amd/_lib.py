@@ -86,6 +86,9 @@ EXPORTS = {
                        ctypes.c_int),
     "ppf_resid_chi2_rows": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, _dp, _dp, _dp,
                              _dp, _dp, _dp, _dp, ctypes.c_double, _dp], ctypes.c_int),
+    "ppf_gaussian_portraits": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                _dp, _dp, ctypes.c_double, ctypes.c_double, _dp, _dp],
+                               ctypes.c_int),
     "ppf_scatter_rotate_rows": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, _dp, _dp, _dp,
                                  _dp], ctypes.c_int),
     "ppf_synth_portraits": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,

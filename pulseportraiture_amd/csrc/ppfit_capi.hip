@@ -42,6 +42,8 @@ struct ppf_ctx {
   Buffer aux;     // misc (synth templates, partial sums)
   Buffer mmean;   // mean template spectra (guess)
   Buffer ptime;   // k_fit_taylor phase clocks (ppf_phase_profile)
+  Buffer spart;   // split scattering solve: block partials + running count
+  int* active_h = nullptr;  // pinned host copy of the running count
   bool phase_prof = false;
   bool timing = false;
   std::vector<TimedLaunch> pending;
@@ -244,6 +246,8 @@ void ppf_ctx_destroy(ppf_ctx* ctx) {
   for (auto p : ctx->tw) if (p) (void)hipFree(p);
   for (auto p : ctx->vp) if (p) (void)hipFree(p);
   if (ctx->ptime.p) (void)hipFree(ctx->ptime.p);
+  if (ctx->spart.p) (void)hipFree(ctx->spart.p);
+  if (ctx->active_h) (void)hipHostFree(ctx->active_h);
   if (ctx->ws.p) (void)hipFree(ctx->ws.p);
   if (ctx->mspec.p) (void)hipFree(ctx->mspec.p);
   if (ctx->aux.p) (void)hipFree(ctx->aux.p);
@@ -456,6 +460,20 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   fa.o_hess = o->hess;
 
   const size_t lds_meta = align256((size_t)nchan * (5 * sizeof(double) + sizeof(int)));
+  // trust-ncg scattering fits: every evaluation split over blocks of >= 64
+  // fitted channels (k_scat_sweep / k_scat_step)
+  static const bool split_on = [] {
+    const char* e = getenv("PPF_SCAT_SPLIT");  // 0: one block per subint (k_solve<true>)
+    return !(e && atoi(e) == 0);
+  }();
+  const bool split_scat = split_on && d->fit_flags[3] && d->method == PPF_METHOD_TRUST_NCG;
+  const int split = std::max(1, std::min(16, nchan / 64));
+  if (split_scat) {
+    if (int r = ensure(ctx, ctx->spart,
+                       (size_t)chunk * ((nchan + 7) / 8) * kScatPart * sizeof(double) + 256))
+      return r;
+    if (!ctx->active_h) HIPCHK(ctx, hipHostMalloc(&ctx->active_h, sizeof(int)));
+  }
   const size_t lds_guess = (size_t)NHP * sizeof(double2);
   for (int64_t s0 = 0; s0 < d->nsub; s0 += chunk) {
     const int nc = (int)std::min<int64_t>(chunk, d->nsub - s0);
@@ -481,9 +499,36 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
           }
           if (exact)
             hipLaunchKernelGGL(k_solve<false>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
-          hipLaunchKernelGGL(k_solve<true>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
+          if (!split_scat)
+            hipLaunchKernelGGL(k_solve<true>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
         }))
       return r;
+    if (split_scat && !tnc) {
+      // k_solve<true> with each evaluation over `split` blocks per subint
+      double* part = static_cast<double*>(ctx->spart.p);
+      int* active = reinterpret_cast<int*>(part + (size_t)nc * ((nchan + 7) / 8) * kScatPart);
+      // the running count is read back every kCheck iterations (a finished
+      // subint's blocks exit at once, so the extra launches are cheap)
+      constexpr int kCheck = 4;
+      for (int it = 0, init = 1;; ++it, init = 0) {
+        if (int r = timed(ctx, PPF_K_SOLVE, [&] {
+              hipLaunchKernelGGL(k_scat_sweep, dim3(nc, split), dim3(kBlock), lds_meta,
+                                 ctx->stream, fa, part, split, init);
+            }))
+          return r;
+        HIPCHK(ctx, hipMemsetAsync(active, 0, sizeof(int), ctx->stream));
+        if (int r = timed(ctx, PPF_K_SOLVE, [&] {
+              hipLaunchKernelGGL(k_scat_step, dim3(nc), dim3(64), 0, ctx->stream, fa, part, split,
+                                 init, active);
+            }))
+          return r;
+        if (it % kCheck != kCheck - 1 && it <= 1001) continue;
+        HIPCHK(ctx, hipMemcpyAsync(ctx->active_h, active, sizeof(int), hipMemcpyDeviceToHost,
+                                   ctx->stream));
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        if (*ctx->active_h == 0 || it > 1001) break;  // trust-ncg stops at 1000 iterations
+      }
+    }
     if (taylor) {
       if (int r = timed(ctx, PPF_K_MOMENTS, [&] {
             const dim3 g(nc, (nchan + 16 * kWaves - 1) / (16 * kWaves));
@@ -695,6 +740,55 @@ int ppf_rotate_accumulate(ppf_ctx* ctx, int32_t nsub, int32_t nchan, int32_t nbi
   return timed(ctx, PPF_K_ROT_ACCUM, [&] {
     hipLaunchKernelGGL(k_accum_reduce, dim3((unsigned)((count + 255) / 256)), dim3(256), 0,
                        ctx->stream, partial, acc, nsplit, count);
+  });
+}
+
+int ppf_gaussian_portraits(ppf_ctx* ctx, int32_t nrow, int32_t nbin, int32_t ngauss,
+                           const int32_t* code, const double* params, double nu_ref, double alpha,
+                           const double* freqs, double* out) {
+  if (!ctx || !code || !params || !freqs || !out) return fail(ctx, PPF_ERR_INVALID, "null argument");
+  if (nrow <= 0) return PPF_OK;
+  if (ngauss < 0 || ngauss > kMaxGauss)
+    return fail(ctx, PPF_ERR_UNSUPPORTED, "ngauss=%d: at most %d components", ngauss, kMaxGauss);
+  for (int i = 0; i < 3; ++i)
+    if (code[i] != 0 && code[i] != 1)
+      return fail(ctx, PPF_ERR_INVALID, "model code digit %d: 0 (power law) or 1 (linear)", code[i]);
+  int logN;
+  if (int r = check_nbin(ctx, nbin, &logN)) return r;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  GaussArgs g;
+  g.nbin = nbin;
+  g.ngauss = ngauss;
+  for (int i = 0; i < 3; ++i) g.code[i] = code[i];
+  // the constants numpy forms on the host (glibc log / sqrt, as numpy's)
+  g.nu_ref = nu_ref;
+  g.lnu = std::log(nu_ref);
+  g.fwhm = 2.0 * std::sqrt(2.0 * std::log(2.0));
+  g.sqrt2pi = std::sqrt(2.0 * M_PI);
+  for (int i = 0; i < 2 + 6 * ngauss; ++i) g.params[i] = params[i];
+  const bool scat = params[1] != 0.0;
+  // gen_gaussian_portrait's scattering branch (pplib.py:915-922): unscattered
+  // rows into a scratch buffer, then scattered into out
+  double* rows = out;
+  double* taus = nullptr;
+  if (scat) {
+    const size_t nb = (size_t)nrow * nbin;
+    if (int r = ensure(ctx, ctx->aux, (nb + (size_t)nrow) * sizeof(double))) return r;
+    rows = static_cast<double*>(ctx->aux.p);
+    taus = rows + nb;
+  }
+  if (int r = timed(ctx, PPF_K_MODEL_FFT, [&] {
+        hipLaunchKernelGGL(k_gauss_port, dim3(nrow), dim3(256), 0, ctx->stream, g, freqs, rows);
+      }))
+    return r;
+  if (!scat) return PPF_OK;
+  const double2* tw;
+  if (int r = twiddles(ctx, nbin, &tw)) return r;
+  return timed(ctx, PPF_K_MODEL_FFT, [&] {
+    hipLaunchKernelGGL(k_scat_taus, dim3((nrow + 255) / 256), dim3(256), 0, ctx->stream, freqs,
+                       nrow, params[1] / (double)nbin, alpha, nu_ref, taus);
+    LOGN_SWITCH(logN, hipLaunchKernelGGL(k_rotate_rows<LG>, dim3(nrow), dim3(kBlock), 0,
+                                         ctx->stream, rows, nullptr, taus, out, tw));
   });
 }
 

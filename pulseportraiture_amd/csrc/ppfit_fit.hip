@@ -540,10 +540,12 @@ __device__ void sweep_taylor0(const FitArgs& a, const Meta& m, const double* prm
 // lrow (optional, kWaves * 8 rows of LDS): each channel lane (h == 0) adds its
 // terms into its own row across groups and the block sums the rows once at
 // the end, instead of NP wave reductions per channel group.
+// [j0, j1) (multiples of 8 but the end): the fitted channels this block sums.
 template <int MODE, bool SCAT>
 __device__ void sweep(const FitArgs& a, const Meta& m, int c, int s, const double* prm,
                       const double* refs, double P, double* acc_slot, double* out,
-                      double (*red)[48], const TaylorSrc& ts, double (*lrow)[48] = nullptr) {
+                      double (*red)[48], const TaylorSrc& ts, double (*lrow)[48] = nullptr,
+                      int j0 = 0, int j1 = 1 << 30, double* gpart = nullptr) {
   if constexpr (MODE == 0 && !SCAT) {
     if (ts.T && ts.same) {
       sweep_taylor0(a, m, prm, acc_slot, out, red, ts);
@@ -563,11 +565,12 @@ __device__ void sweep(const FitArgs& a, const Meta& m, int c, int s, const doubl
   if (lrow && h == 0)
     for (int i = 0; i < NP; ++i) myrow[i] = 0.0;
   __syncthreads();
-  const int ngroups = (m.nok + 7) >> 3;
-  for (int gi = w; gi < ngroups; gi += kWaves) {
+  const int jend = min(m.nok, j1);
+  const int ngroups = (jend + 7) >> 3;
+  for (int gi = (j0 >> 3) + w; gi < ngroups; gi += kWaves) {
     const int j = gi * 8 + g8;
-    const bool valid = j < m.nok;
-    const int jj = valid ? j : m.nok - 1;
+    const bool valid = j < jend;
+    const int jj = valid ? j : jend - 1;
     const int n = m.chan[jj];
     const double fr = m.fr[jj];
     double acc[NACC];
@@ -638,7 +641,10 @@ __device__ void sweep(const FitArgs& a, const Meta& m, int c, int s, const doubl
 #pragma unroll
       for (int i = 0; i < NP; ++i) {
         const double v = wave_sum(ct[i]);  // only h == 0 lanes hold terms
-        if (lane == 0) red[w][i] += v;
+        if (lane == 0) {
+          if (gpart) gpart[(size_t)gi * kScatPart + i] = v;  // summed by the caller
+          else red[w][i] += v;
+        }
       }
     }
   }
@@ -694,6 +700,7 @@ __device__ void guess_subint(const FitArgs& a, int c, int s, unsigned char* dyn,
     st.scat_post = st.scat;
     st.taylor = !st.scat && a.T != nullptr;
     st.kit = 0;
+    st.sdone = 0;
     st.phase = 0;
     st.fin = 0;
     st.mvalid = 0;
@@ -973,6 +980,173 @@ __global__ __launch_bounds__(kBlock) void k_solve(FitArgs a) {
     st.slot = sh.slot;
     const double tl = a.log10_tau ? pow(10.0, sh.x[3]) : sh.x[3];
     st.scat_post = SCAT && tl != 0.0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Split scattering solve: k_solve<true>'s trust-ncg with every evaluation
+// spread over `split` workgroups per subint.  One exact scattering sweep of a
+// 512-channel subint is ~4 MB of X; a single workgroup streaming it nfev
+// times ran at 0.2 of HBM (r02 config 3).  Per iteration the host launches
+//   k_scat_sweep (subint x split blocks): partial f, g, H over a channel
+//     range at the subint's point (x at init, else the proposal xp), and the
+//     per-channel accumulators into the proposal's slot;
+//   k_scat_step (one wave per subint): the per-group terms summed in the
+//     order one k_solve block sums them, then k_solve's accept / reject and
+//     the next Steihaug proposal, with the solver state kept in SolveState
+//     between launches;
+// until no subint is left running.  Every sum is formed in k_solve<true>'s
+// order, so the trajectory, nfev, status and result are bitwise k_solve's.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool scat_split_owner(const FitArgs& a, const SolveState& st) {
+  return a.method == PPF_METHOD_TRUST_NCG && st.scat != 0 && !st.sdone;
+}
+
+__global__ __launch_bounds__(kBlock) void k_scat_sweep(FitArgs a, double* part, int split,
+                                                       int init) {
+  extern __shared__ __align__(16) unsigned char dyn[];
+  __shared__ SolveShared sh;
+  const int c = blockIdx.x, q = blockIdx.y, s = a.sub0 + c, tid = threadIdx.x;
+  const SolveState& st = a.st[c];
+  if (!scat_split_owner(a, st)) return;
+  const Meta m = load_meta(a, c, s, dyn, &sh.nok);
+  if (m.nok == 0) return;
+  // channel range of this block: whole groups of 8, blocks in order; each
+  // group's wave-reduced terms go to part[c][group] (k_scat_step sums them
+  // in k_solve's order)
+  const int ng = (m.nok + 7) >> 3;
+  const int per = (ng + split - 1) / split;
+  const int j0 = q * per * 8, j1 = min(m.nok, (q + 1) * per * 8);
+  const double* prm = init ? st.x : st.xp;
+  const int slot = init ? 0 : (st.slot ^ 1);
+  double* acc = a.acc + ((size_t)c * 2 + slot) * a.nchan * NACC;
+  if (j0 < j1)
+    sweep<0, true>(a, m, c, s, prm, st.refs, a.P[s], acc, sh.out, sh.red, TaylorSrc{}, nullptr,
+                   j0, j1, part + (size_t)c * ((a.nchan + 7) >> 3) * kScatPart);
+}
+
+__global__ __launch_bounds__(64) void k_scat_step(FitArgs a, const double* part, int split,
+                                                  int init, int* active) {
+  __shared__ double out[kScatPart];
+  const int c = blockIdx.x, s = a.sub0 + c, lane = threadIdx.x;
+  SolveState& st = a.st[c];
+  if (!scat_split_owner(a, st)) return;
+  double cnt = 0.0;  // fitted channels
+  for (int n = lane; n < a.nchan; n += 64) cnt += (!a.mask || a.mask[(size_t)s * a.nchan + n]) ? 1.0 : 0.0;
+  const int nok = (int)wave_sum(cnt);
+  // group terms summed exactly as one k_solve block sums them: wave w's
+  // running sum over groups w, w + kWaves, ..., then the waves in order
+  if (lane < 21) {
+    const double* pc = part + (size_t)c * ((a.nchan + 7) >> 3) * kScatPart;
+    const int ng = (nok + 7) >> 3;
+    double t = 0.0;
+    for (int w = 0; w < kWaves; ++w) {
+      double r = 0.0;
+      for (int gi = w; gi < ng; gi += kWaves) r += pc[(size_t)gi * kScatPart + lane];
+      t += r;
+    }
+    out[lane] = t;
+  }
+  __syncthreads();
+  auto load_fgh = [&](double& ff, double& gg, double (&HH)[5]) {
+    ff = out[0];
+    gg = lane < 5 ? out[1 + lane] : 0.0;
+#pragma unroll
+    for (int p = 0; p < 15; ++p) {
+      const double v = out[6 + p];
+      if (lane == pair_i(p)) HH[pair_j(p)] = v;
+      if (lane == pair_j(p)) HH[pair_i(p)] = v;
+    }
+  };
+  double f, g, xl, Hrow[5] = {0, 0, 0, 0, 0}, tr, predv, pl;
+  int hits, k, status, nfev, slot;
+  bool done = false;
+  if (init) {
+    load_fgh(f, g, Hrow);
+    xl = lane < 5 ? st.x[lane] : 0.0;
+    tr = 1.0;
+    predv = pl = 0.0;
+    hits = k = status = 0;
+    nfev = 1;
+    slot = 0;
+    if (nok == 0) { status = -1; nfev = 0; done = true; }
+    if (a.solver_flags & PPF_SOLVE_EVAL) { status = 1; done = true; }
+  } else {
+    f = st.fun;
+    g = lane < 5 ? st.g[lane] : 0.0;
+    if (lane < 5)
+      for (int j = 0; j < 5; ++j) Hrow[j] = st.H[lane * 5 + j];
+    xl = lane < 5 ? st.x[lane] : 0.0;
+    tr = st.tr;
+    predv = st.predv;
+    pl = lane < 5 ? st.pl[lane] : 0.0;
+    hits = st.hits;
+    k = st.kit;
+    status = st.status;
+    nfev = st.nfev;
+    slot = st.slot;
+    // k_solve's post-sweep block
+    double fp, gp, Hp[5] = {0, 0, 0, 0, 0};
+    load_fgh(fp, gp, Hp);
+    nfev += 1;
+    const double actual = f - fp;
+    const double pred = f - predv;
+    if (pred <= 0.0) {
+      status = 2;
+      done = true;
+    } else {
+      const double rho = actual / pred;
+      if (rho < 0.25) tr *= 0.25;
+      else if (rho > 0.75 && hits) tr = fmin(2.0 * tr, 1000.0);
+      if (rho > 0.15) {
+        xl = xl + pl;
+        f = fp;
+        g = gp;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) Hrow[j] = Hp[j];
+        slot ^= 1;
+      }
+      k += 1;
+      if (k >= 1000) { status = 1; done = true; }
+    }
+  }
+  if (!done) {  // k_solve's loop head: NaN gradient, else the next proposal
+    const double jm = sqrt(dot8(g, g));
+    if (!(jm >= -1.0)) {
+      status = 0;
+      done = true;
+    } else {
+      pl = steihaug(f, g, Hrow, tr, hits);
+      predv = model_val(f, g, Hrow, pl);
+    }
+  }
+  // state back (lanes < 5 own the vectors; lane 0 the scalars)
+  if (lane < 5) {
+    st.x[lane] = xl;
+    st.g[lane] = g;
+    for (int j = 0; j < 5; ++j) st.H[lane * 5 + j] = Hrow[j];
+    st.pl[lane] = pl;
+    st.xp[lane] = xl + pl;
+  }
+  if (done && lane < 5) store_grad_hess(a, s, lane, nok > 0, g, Hrow);
+  if (lane == 0) {
+    st.fun = nok ? f : NAN;
+    st.tr = tr;
+    st.predv = predv;
+    st.hits = hits;
+    st.kit = k;
+    st.status = status;
+    st.nfev = nok ? nfev : 0;
+    st.slot = slot;
+    if (done) st.sdone = 1;
+    else atomicAdd(active, 1);
+  }
+  if (done) {
+    const double x3 = __shfl(xl, 3);
+    if (lane == 0) {
+      const double tl = a.log10_tau ? pow(10.0, x3) : x3;
+      st.scat_post = tl != 0.0;
+    }
   }
 }
 

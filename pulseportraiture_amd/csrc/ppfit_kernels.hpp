@@ -64,6 +64,10 @@ struct SolveState {
   double g[5], H[25], tr;
   int nfev, status, slot, scat, scat_post, taylor;
   int kit, phase, fin, mvalid, xslot, wslot;
+  // split scattering solve (k_scat_sweep / k_scat_step): the proposal, its
+  // step and predicted value, the Steihaug boundary flag, done
+  double xp[5], pl[5], predv;
+  int hits, sdone;
 };
 
 struct FitArgs {
@@ -370,6 +374,15 @@ __device__ inline void guess_search(const double2* rm, int NH, double ie2, int N
   __syncthreads();
 }
 
+constexpr int kMaxGauss = 32;
+struct GaussArgs {
+  int nbin, ngauss;
+  int code[3];              // evolution of loc / wid / amp: 0 power law, 1 linear
+  double nu_ref, lnu;       // reference frequency and its log (host numpy)
+  double fwhm, sqrt2pi;     // 2 sqrt(2 ln 2), sqrt(2 pi) as numpy forms them
+  double params[2 + 6 * kMaxGauss];  // DC, TAU, then loc, dloc, wid, dwid, amp, damp
+};
+
 struct ResidArgs {
   const double* data;      // [nrow][nbin]
   const double* phase;     // [nrow] or NULL
@@ -408,7 +421,13 @@ __global__ void k_rot_accum(const double* data, const double* phase, const doubl
 __global__ void k_accum_reduce(const double2* partial, double2* accum, int nsplit, size_t count);
 template <int LOGN> __global__ void k_resid_chi2(ResidArgs a, const double2* tw);
 __global__ void k_vpow(double2* vp, int N, int rows);
+__global__ void k_gauss_port(GaussArgs g, const double* freqs, double* out);
+__global__ void k_scat_taus(const double* freqs, int n, double tau, double alpha, double nu_ref,
+                            double* out);
 __global__ void k_guess(FitArgs a);
+constexpr int kScatPart = 24;  // split scattering sweep partial: f, g[5], H pairs[15], pad
+__global__ void k_scat_sweep(FitArgs a, double* part, int split, int init);
+__global__ void k_scat_step(FitArgs a, const double* part, int split, int init, int* active);
 __global__ void k_model_mean(const double2* M, double2* Mmean, int nchan, int NHP);
 __global__ void k_fit_taylor(FitArgs a);
 template <int U>

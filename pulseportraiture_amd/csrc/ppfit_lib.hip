@@ -3,4 +3,5 @@
 #include "ppfit_fit.hip"
 #include "ppfit_taylor.hip"
 #include "ppfit_tnc.hip"
+#include "ppfit_models.hip"
 #include "ppfit_capi.hip"

@@ -442,12 +442,15 @@ __global__ __launch_bounds__(kBlock) void k_rotate_rows(const double* __restrict
   load_row<LOGN>(buf, in + (size_t)r * 2 * N);
   __syncthreads();
   lds_fft<LOGN, false>(buf, tw);
-  const double ph = phase[r];
+  const double ph = phase ? phase[r] : 0.0;
   double2 xs[(N + kBlock) / kBlock + 1];
 #pragma unroll
   for (int i = 0; i < KI; ++i) {
     const int k = threadIdx.x + i * kBlock;
-    if (k <= N) xs[i] = cmul(rfft_post<LOGN>(buf, k, tw), turn_phasor((double)k, ph));
+    if (k <= N) {
+      xs[i] = rfft_post<LOGN>(buf, k, tw);
+      if (phase) xs[i] = cmul(xs[i], turn_phasor((double)k, ph));
+    }
   }
   const double t2 = tau ? 2.0 * M_PI * tau[r] : 0.0;
   if (t2 != 0.0) {  // scattering_portrait_FT: x / (1 + 2 pi i k tau)

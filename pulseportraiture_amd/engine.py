@@ -275,6 +275,26 @@ class Engine:
         out._keep = (r, ph)
         return out.reshape(shape)
 
+    def gaussian_portraits(self, model_code, params, scattering_index, nbin, freqs, nu_ref):
+        """gen_gaussian_portrait (pplib.py:853-930) on the device for every row
+        of freqs ([..., nchan]); params as gen_gaussian_portrait takes them
+        (TAU already in bins).  Returns a device tensor [..., nchan, nbin]."""
+        dev = self.device
+        f = _dev_f64(freqs, dev)
+        shape = tuple(f.shape)
+        f = f.reshape(-1).contiguous()
+        params = np.asarray(params, dtype=np.float64)
+        ngauss = (len(params) - 2) // 6
+        code = (ctypes.c_int32 * 3)(*[int(c) for c in str(model_code)[:3]])
+        par = (ctypes.c_double * len(params))(*params.tolist())
+        out = torch.empty((f.numel(), nbin), dtype=torch.float64, device=dev)
+        self._chk(self.lib.ppf_gaussian_portraits(
+            self.ctx, f.numel(), nbin, ngauss, ctypes.cast(code, ctypes.c_void_p),
+            ctypes.cast(par, ctypes.c_void_p), float(nu_ref), float(scattering_index), _ptr(f),
+            _ptr(out)))
+        out._keep = (f,)
+        return out.reshape(shape + (nbin,))
+
     def irfft_rows(self, spec, nbin):
         dev = self.device
         if isinstance(spec, torch.Tensor) and spec.is_complex():

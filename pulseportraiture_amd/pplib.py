@@ -208,6 +208,31 @@ def read_model(modelfile, phases=None, freqs=None, P=None, quiet=False):
     return (name, ngauss, model)
 
 
+def gen_gaussian_portraits_device(model_code, params, scattering_index, nbin, freqs, nu_ref):
+    """gen_gaussian_portrait (pplib.py:853-930) for rows of frequencies
+    ([..., nchan]) in one device call (ppf_gaussian_portraits); returns a
+    numpy array [..., nchan, nbin].  params[1] (TAU) in bins, as there."""
+    from .engine import get_engine
+    return get_engine().gaussian_portraits(model_code, params, scattering_index, nbin, freqs,
+                                           nu_ref).cpu().numpy()
+
+
+def read_model_device(modelfile, nbin, freqs, P=None, quiet=False):
+    """read_model(modelfile, phases, freqs, P) (pplib.py:2873-2959) with the
+    portrait built on the device for every row of freqs ([..., nchan]): the
+    .gmodel parse, TAU *= nbin / P, then gen_gaussian_portraits_device.
+    Returns (name, ngauss, model [..., nchan, nbin])."""
+    name, code, nu_ref, ngauss, params, flags, alpha, fit_alpha = read_model(modelfile,
+                                                                             quiet=True)
+    params = np.array(params, dtype=float)
+    if params[1] != 0:
+        if P is None:
+            print("Need period P for non-zero scattering value TAU.")
+            return 0
+        params[1] *= nbin / P
+    return name, ngauss, gen_gaussian_portraits_device(code, params, alpha, nbin, freqs, nu_ref)
+
+
 def write_model(filename, name, model_code, nu_ref, model_params, fit_flags, alpha,
                 fit_alpha, append=False, quiet=False):
     """pplib.py:2834-2871 (same text layout)."""

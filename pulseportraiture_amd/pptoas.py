@@ -14,7 +14,8 @@ import numpy as np
 from . import archive as _arch
 from .mjd import MJD
 from .pplib import (DataBunch, F0_fact, phase_transform, guess_fit_freq, read_model,
-                    gen_gaussian_portrait, scattering_alpha, weighted_mean, write_TOAs)
+                    read_model_device, gen_gaussian_portraits_device, scattering_alpha,
+                    weighted_mean, write_TOAs)
 from .pptoaslib import fit_portraits_batch, report_failure
 
 max_nfile = 999
@@ -104,22 +105,39 @@ class GetTOAs:
         if fit_scat:
             self.model_code, self.model_nu_ref = code, nu_ref
             self.gparams, self.alpha = gparams, alpha
-        cache, models, idx = {}, [], np.zeros(nsub, dtype=np.int32)
+        # one template per distinct (freqs, P-if-scattered) key, all built on
+        # the device (ppf_gaussian_portraits): read_model per subint in the
+        # reference (pptoas.py:351-378); fit_scat builds the unscattered one
+        cache, keyf, keyP, idx = {}, [], [], np.zeros(nsub, dtype=np.int32)
+        tau_P = gparams[1] != 0 and not fit_scat
         for isub in data.ok_isubs:
             P = data.Ps[isub]
             f = data.freqs[isub]
-            key = (f.tobytes(), P if (gparams[1] != 0 and not fit_scat) else None)
+            key = (f.tobytes(), P if tau_P else None)
             if key not in cache:
-                if not fit_scat:
-                    m = read_model(self.modelfile, data.phases, f, P, quiet=True)[2]
-                else:
-                    up = np.copy(gparams)
-                    up[1] = 0.0
-                    m = gen_gaussian_portrait(code, up, 0.0, data.phases, f, nu_ref)
-                cache[key] = len(models)
-                models.append(m)
+                cache[key] = len(keyf)
+                keyf.append(f)
+                keyP.append(P)
             idx[isub] = cache[key]
-        return np.array(models), idx, None
+        nbin = len(data.phases)
+        models = np.empty((len(keyf), data.nchan, nbin))
+        params = np.array(gparams, dtype=float)
+        if fit_scat:
+            params[1] = 0.0
+            models[:] = gen_gaussian_portraits_device(code, params, 0.0, nbin, np.array(keyf),
+                                                      nu_ref)
+        elif not tau_P:
+            models[:] = gen_gaussian_portraits_device(code, params, alpha, nbin, np.array(keyf),
+                                                      nu_ref)
+        else:  # read_model's TAU * nbin / P differs per period
+            for P in sorted(set(keyP)):
+                sel = [i for i, q in enumerate(keyP) if q == P]
+                pp = np.copy(params)
+                pp[1] *= nbin / P
+                models[sel] = gen_gaussian_portraits_device(code, pp, alpha, nbin,
+                                                            np.array([keyf[i] for i in sel]),
+                                                            nu_ref)
+        return models, idx, None
 
     def get_TOAs(self, datafile=None, tscrunch=False, nu_refs=None, DM0=None, bary=True,
                  fit_DM=True, fit_GM=False, fit_scat=False, log10_tau=True, scat_guess=None,
@@ -298,8 +316,8 @@ class GetTOAs:
                     f = data.freqs[isub]
                     key = midx.setdefault((f.tobytes(), data.Ps[isub]), len(models))
                     if key == len(models):
-                        models.append(read_model(self.modelfile, get_bin_centers(nbin), f,
-                                                 data.Ps[isub], quiet=True)[2])
+                        models.append(read_model_device(self.modelfile, nbin, f, data.Ps[isub],
+                                                        quiet=True)[2])
                 for ichan in data.ok_ichans[isub]:
                     if mweights is not None and mweights[ichan] == 0:
                         continue
@@ -432,10 +450,10 @@ class GetTOAs:
                     info = read_model(self.modelfile, quiet=True)
                     gparams = np.copy(info[4])
                     gparams[1] = 0.0
-                    m = gen_gaussian_portrait(info[1], gparams, 0.0, data.phases, freqs, info[2])
+                    m = gen_gaussian_portraits_device(info[1], gparams, 0.0, nbin, freqs, info[2])
                 else:
-                    m = read_model(self.modelfile, data.phases, freqs, data.Ps.mean(),
-                                   quiet=True)[2]
+                    m = read_model_device(self.modelfile, nbin, freqs, data.Ps.mean(),
+                                          quiet=True)[2]
                 models.append(np.asarray(m, dtype=np.float64))
             k = mkeys[key]
             phs = phase_shifts(phi, DM, GM, freqs, nu_ref_DM, nu_ref_GM, P)

@@ -560,9 +560,41 @@ def gen_zap(pplib, pptoaslib, pptoas, ppzap):
     MG.save("zap.npz", **out)
 
 
+# --------------------------------------------------------------------------
+# Template portraits (gen_gaussian_portrait / read_model, pplib.py:853-930,
+# 2873-2959) for the device generator: the headline shape with Doppler-
+# shifted channel frequencies, both evolution codes, and a scattered model.
+# --------------------------------------------------------------------------
+MODEL_CASES = [  # name, nchan, nbin, CODE, TAU [s], freq scale
+    ("hl", 64, 2048, "000", 0.0, 1.0001),
+    ("lin", 32, 512, "101", 0.0, 1.0),
+    ("lin2", 16, 256, "011", 0.0, 0.9999),
+    ("scat", 128, 1024, "000", 0.0003, 1.0),
+]
+
+
+def gen_models_r2(pplib):
+    import tempfile
+    out = {}
+    src = open(MG.GMODEL).read()
+    for name, nchan, nbin, code, tau, scale in MODEL_CASES:
+        txt = src.replace("CODE    000", "CODE    " + code).replace(
+            "TAU     0.00000000 1", "TAU     %.8f 1" % tau)
+        path = os.path.join(tempfile.mkdtemp(), name + ".gmodel")
+        open(path, "w").write(txt)
+        freqs = MG.channel_freqs(nchan) * scale
+        phases = pplib.get_bin_centers(nbin)
+        _, _, model = pplib.read_model(path, phases, freqs, P0, quiet=True)
+        out[name + "_freqs"] = freqs
+        out[name + "_model"] = model
+        out[name + "_gmodel"] = np.frombuffer(txt.encode(), dtype=np.uint8)
+        print("model %s: %s, max %.6g" % (name, model.shape, np.max(np.abs(model))))
+    MG.save("models_r2.npz", **out)
+
+
 def main():
     what = sys.argv[1:] or ["fit", "configs", "align", "headline", "timing", "tncfloor",
-                            "narrowband", "zap"]
+                            "narrowband", "zap", "models"]
     np.seterr(all="ignore")
     if "headline" in what:
         gen_headline_2k()
@@ -584,6 +616,8 @@ def main():
             gen_tnc_floor(pplib, pptoaslib)
         if "narrowband" in rest:
             gen_narrowband(pplib, pptoaslib, pptoas)
+        if "models" in rest:
+            gen_models_r2(pplib)
         if "zap" in rest:
             import ppzap
             gen_zap(pplib, pptoaslib, pptoas, ppzap)

@@ -82,6 +82,10 @@ def run_get_toas(log):
         k["log_calls"] = log
         return fake_fit(*a, **k)
     pptoas.fit_portraits_batch = fit
+    # templates: the host restatement in place of the device generator
+    pptoas.gen_gaussian_portraits_device = lambda code, params, alpha, nbin, freqs, nu_ref: \
+        np.array([pplib.gen_gaussian_portrait(code, params, alpha, pplib.get_bin_centers(nbin), f,
+                                              nu_ref) for f in np.atleast_2d(freqs)])
     gt = pptoas.GetTOAs(names, synth.EXAMPLE_GMODEL, quiet=True)
     gt.get_TOAs(quiet=True)
     return [pplib.toa_line(t) for t in gt.TOA_list], gt
