@@ -45,9 +45,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 FP64_PEAK_TFLOPS = 78.6  # AMD MI355X spec, fp64 vector = fp64 matrix (not in the guide's table)
 # HBM bytes per subint per kernel from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
 # passes over this same bench (tools/profile_r1.sh + tools/pmc_summary.py).
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
 KERNEL_SYMBOL = {"solve": "k_solve<false>", "data_xspec": "k_data_xspec<10>",
-                 "post": "k_post<false>", "guess": "k_guess", "moments": "k_moments<16>",
+                 "post": "k_post<false>", "guess": "k_guess", "moments": "k_moments<8>",
                  "fit_taylor": "k_fit_taylor"}
 
 
