@@ -242,6 +242,67 @@ class Engine:
         return out
 
     # -- other hot-path entry points ---------------------------------------
+    def fit_batch_streamed(self, host_data, model, freqs, P, init, fit_flags, chunk=2048, **kw):
+        """fit_batch over host-resident subints [nsub, nchan, nbin] that need
+        not fit in HBM: chunk i + 1 is copied host -> device on a second
+        stream while chunk i is fitted on the context stream (two device
+        buffers).  host_data should be a pinned torch CPU tensor for full
+        PCIe rate (an unpinned one is copied synchronously).  Per-subint
+        arguments (leading dimension nsub) are sliced per chunk; results are
+        those of one fit_batch call over all subints, concatenated on the
+        device."""
+        dev = self.device
+        hd = host_data if isinstance(host_data, torch.Tensor) else torch.from_numpy(
+            np.ascontiguousarray(host_data, dtype=np.float64))
+        nsub, nchan, nbin = hd.shape
+        chunk = max(1, min(int(chunk), nsub))
+
+        def part(v, s0, s1):
+            if v is None or np.ndim(v) == 0:
+                return v
+            if isinstance(v, (list, tuple)) and not len(v):
+                return v
+            a = v if isinstance(v, torch.Tensor) else np.asarray(v)
+            return a[s0:s1] if a.shape[0] == nsub and nsub > 1 else a
+
+        per_sub = ["nu_fit", "nu_out", "errs", "chan_mask", "weights", "model_idx", "guess_nu",
+                   "guess_tau"]
+        comp = self.stream
+        copy = torch.cuda.Stream(dev)
+        bufs = [torch.empty((chunk, nchan, nbin), dtype=torch.float64, device=dev)
+                for _ in range(2)]
+        copied = [torch.cuda.Event() for _ in range(2)]
+        free = [torch.cuda.Event() for _ in range(2)]
+        nchunks = (nsub + chunk - 1) // chunk
+
+        def issue(i):
+            s0 = i * chunk
+            n = min(chunk, nsub - s0)
+            with torch.cuda.stream(copy):
+                if i >= 2:
+                    copy.wait_event(free[i % 2])  # chunk i - 2 is done with the buffer
+                bufs[i % 2][:n].copy_(hd[s0:s0 + n], non_blocking=True)
+                copied[i % 2].record(copy)
+
+        outs = []
+        issue(0)
+        for i in range(nchunks):
+            s0 = i * chunk
+            s1 = min(nsub, s0 + chunk)
+            if i + 1 < nchunks:
+                issue(i + 1)
+            comp.wait_event(copied[i % 2])
+            kwi = dict(kw)
+            for k in per_sub:
+                if k in kwi:
+                    kwi[k] = part(kwi[k], s0, s1)
+            r = self.fit_batch(bufs[i % 2][:s1 - s0], model, part(freqs, s0, s1),
+                               part(P, s0, s1), part(init, s0, s1), fit_flags, **kwi)
+            free[i % 2].record(comp)
+            outs.append(r)
+        return {k: torch.cat([o[k] for o in outs]) for k in outs[0]
+                if isinstance(outs[0][k], torch.Tensor)}
+
     def phase_shift_batch(self, data, model, noise=None, Ns=100, bounds=(-0.5, 0.5),
                           model_idx=None):
         """fit_phase_shift over rows (pplib.py:2054-2100) -> [nprof, 6] device tensor."""
