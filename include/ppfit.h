@@ -18,6 +18,9 @@
  *                              ppalign.py:202-208
  *   ppf_irfft_rows          <- numpy.fft.irfft (final step of ppalign.py:210-213)
  *   ppf_noise_rows          <- pplib.get_noise_PS(chans=True)  pplib.py:2227-2253
+ *   ppf_unpack_subints      <- PSRCHIVE Archive_load + pscrunch in
+ *                              pplib.load_data  pplib.py:2670-2732 (with
+ *                              include/ppfits.h, the host PSRFITS reader)
  *   ppf_gaussian_portraits  <- pplib.gen_gaussian_portrait / read_model
  *                              pplib.py:853-930, 2873-2959
  *   ppf_scatter_rotate_rows <- GetTOAs.show_fit port/model  pptoas.py:1389-1402
@@ -72,7 +75,8 @@ extern "C" {
 #define PPF_K_FIT_TAYLOR 11
 #define PPF_K_MOMENTS 12
 #define PPF_K_RESID 13
-#define PPF_NUM_KERNELS 14
+#define PPF_K_UNPACK 14
+#define PPF_NUM_KERNELS 15
 
 typedef struct ppf_ctx ppf_ctx;
 
@@ -219,6 +223,16 @@ int ppf_rotate_accumulate(ppf_ctx* ctx, int32_t nsub, int32_t nchan,
 int ppf_gaussian_portraits(ppf_ctx* ctx, int32_t nrow, int32_t nbin, int32_t ngauss,
                            const int32_t* code, const double* params, double nu_ref,
                            double alpha, const double* freqs, double* out);
+
+/* PSRFITS samples to physical values (PSRCHIVE's load + pscrunch in
+ * load_data, pplib.py:2670-2732): raw [nsub][npol][nchan][nbin] of
+ * raw_type (ppfits.h PPFITS_RAW_*: 1 uint8, 2 int16, 3 float32), scl and
+ * offs [nsub][npol][nchan] (DAT_SCL, DAT_OFFS); value = raw * scl + offs.
+ * pmode 0 keeps every polarisation, 1 sums the first two (AA + BB), 2 takes
+ * the first (Stokes I); out [nsub][pmode ? 1 : npol][nchan][nbin].        */
+int ppf_unpack_subints(ppf_ctx* ctx, int32_t nsub, int32_t npol, int32_t nchan, int32_t nbin,
+                       int32_t raw_type, const void* raw, const double* scl, const double* offs,
+                       int32_t pmode, double* out);
 
 /* out[r] = irfft(rfft(in[r]) e^{2 pi i k phase[r]} / (1 + 2 pi i k tau[r]))
  * (rotate_portrait_full of a scattered template, pptoas.py:1389-1397);

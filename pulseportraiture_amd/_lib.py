@@ -19,7 +19,7 @@ METHODS = {"trust-ncg": PPF_METHOD_TRUST_NCG, "TNC": PPF_METHOD_TNC,
            "Newton-CG": PPF_METHOD_NEWTON_CG, "TNC-legacy": PPF_METHOD_TNC_LEGACY}
 KERNEL_IDS = {"model_fft": 0, "data_xspec": 1, "solve": 2, "phase_shift": 3,
               "rotate": 4, "rot_accum": 5, "synth": 6, "irfft": 7, "noise": 8,
-              "guess": 9, "post": 10, "fit_taylor": 11, "moments": 12, "resid": 13}
+              "guess": 9, "post": 10, "fit_taylor": 11, "moments": 12, "resid": 13, "unpack": 14}
 PPF_SOLVE_EXACT = 1
 PPF_SOLVE_EVAL = 2
 PPF_GUESS_DIRECT = 4
@@ -86,6 +86,9 @@ EXPORTS = {
                        ctypes.c_int),
     "ppf_resid_chi2_rows": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, _dp, _dp, _dp,
                              _dp, _dp, _dp, _dp, ctypes.c_double, _dp], ctypes.c_int),
+    "ppf_unpack_subints": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                            ctypes.c_int32, ctypes.c_int32, _dp, _dp, _dp, ctypes.c_int32, _dp],
+                           ctypes.c_int),
     "ppf_gaussian_portraits": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                 _dp, _dp, ctypes.c_double, ctypes.c_double, _dp, _dp],
                                ctypes.c_int),

@@ -1,10 +1,12 @@
-"""Archive access for the drivers (stand-in for pplib.load_data, pplib.py:2650-2820).
+"""Archive access for the drivers (pplib.load_data, pplib.py:2650-2820).
 
-PSRCHIVE is not part of this build, so
-archives reach the drivers either as in-memory DataBunches with the keys of
-pplib.py:2809-2819, registered under a name, or as ``.npz`` archives written
-by ``save_archive``.  Anything else raises RuntimeError, which the drivers
-treat exactly like a failed PSRCHIVE load (skip the archive, pptoas.py:271).
+PSRCHIVE is not part of this build.  Archives reach the
+drivers as fold-mode PSRFITS files (psrfits.py: the native reader of
+include/ppfits.h plus device unpacking, §8(f) next #1), as in-memory
+DataBunches with the keys of pplib.py:2809-2819 registered under a name, or
+as ``.npz`` archives written by ``save_archive``.  Anything else raises
+RuntimeError, which the drivers treat exactly like a failed PSRCHIVE load
+(skip the archive, pptoas.py:271).
 """
 import os
 
@@ -93,12 +95,28 @@ def save_archive(path, bunch):
     return path
 
 
+def is_fits(filename):
+    """A FITS file on disk (the 'SIMPLE  =' card that opens every FITS file)."""
+    try:
+        with open(filename, "rb") as f:
+            return f.read(9) == b"SIMPLE  ="
+    except (OSError, TypeError):
+        return False
+
+
 def load_data(filename, **kw):
-    """Archive by name: registered bunch, else an .npz written by save_archive."""
+    """Archive by name: registered bunch, an .npz written by save_archive, or a
+    fold-mode PSRFITS file (psrfits.load_psrfits: host reader + device unpack)."""
     if isinstance(filename, dict):
         return normalize(filename)
     if filename in _registry:
         return _registry[filename]
+    if isinstance(filename, str) and is_fits(filename):
+        from .psrfits import load_psrfits
+        return normalize(load_psrfits(filename, pscrunch=kw.get("pscrunch", False),
+                                      dededisperse=kw.get("dededisperse", False),
+                                      tscrunch=kw.get("tscrunch", False),
+                                      quiet=kw.get("quiet", True)), filename)
     if isinstance(filename, str) and os.path.exists(filename) and filename.endswith(".npz"):
         z = np.load(filename, allow_pickle=False)
         b = {k: z[k] for k in z.files if not k.startswith("meta_") and k != "epochs"}
@@ -111,15 +129,15 @@ def load_data(filename, **kw):
             if k in b:
                 b[k] = int(b[k])
         return normalize(b, filename)
-    raise RuntimeError("Cannot load_data(%s): PSRCHIVE archives are not supported "
-                       "by this build; use a registered or .npz archive" % filename)
+    raise RuntimeError("Cannot load_data(%s): not a registered, .npz or PSRFITS archive "
+                       "(other PSRCHIVE formats need PSRCHIVE)" % filename)
 
 
 def file_is_type(filename, filetype="ASCII"):
     """Stand-in for pplib.file_is_type (pplib.py:3021-3037) without `file -L`."""
     if filetype == "ASCII":
         if not isinstance(filename, str) or filename in _registry or \
-                not os.path.isfile(filename) or filename.endswith(".npz"):
+                not os.path.isfile(filename) or filename.endswith(".npz") or is_fits(filename):
             return False
         try:
             with open(filename) as f:
@@ -128,5 +146,6 @@ def file_is_type(filename, filetype="ASCII"):
         except (UnicodeDecodeError, OSError):
             return False
     if filetype == "FITS":
-        return isinstance(filename, str) and (filename in _registry or filename.endswith(".npz"))
+        return isinstance(filename, str) and (filename in _registry or filename.endswith(".npz")
+                                              or is_fits(filename))
     return False

@@ -21,7 +21,27 @@ def needs_build():
     return any(os.path.getmtime(s) > t for s in srcs)
 
 
+# host-only PSRFITS reader (include/ppfits.h): plain C++, loadable without a GPU
+FITS_OUT = os.path.join(HERE, "libppfits.so")
+FITS_SRC = [os.path.join(CSRC, "psrfits.cpp"), os.path.join(ROOT, "include", "ppfits.h")]
+CXX = os.environ.get("CXX", "g++")
+
+
+def build_fits(force=False, verbose=False):
+    if not force and os.path.exists(FITS_OUT) and \
+            all(os.path.getmtime(s) <= os.path.getmtime(FITS_OUT) for s in FITS_SRC):
+        return FITS_OUT
+    cmd = [CXX, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall",
+           "-I" + os.path.join(ROOT, "include"), FITS_SRC[0], "-o", FITS_OUT + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd)
+    os.replace(FITS_OUT + ".tmp", FITS_OUT)
+    return FITS_OUT
+
+
 def build(force=False, verbose=False):
+    build_fits(force, verbose)
     if not force and not needs_build():
         return OUT
     cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",

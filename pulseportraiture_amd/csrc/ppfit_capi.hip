@@ -792,6 +792,39 @@ int ppf_gaussian_portraits(ppf_ctx* ctx, int32_t nrow, int32_t nbin, int32_t nga
   });
 }
 
+int ppf_unpack_subints(ppf_ctx* ctx, int32_t nsub, int32_t npol, int32_t nchan, int32_t nbin,
+                       int32_t raw_type, const void* raw, const double* scl, const double* offs,
+                       int32_t pmode, double* out) {
+  if (!ctx || !raw || !scl || !offs || !out) return fail(ctx, PPF_ERR_INVALID, "null argument");
+  if (nsub <= 0) return PPF_OK;
+  if (npol <= 0 || nchan <= 0 || nbin <= 0) return fail(ctx, PPF_ERR_INVALID, "bad shape");
+  if (raw_type < 1 || raw_type > 3) return fail(ctx, PPF_ERR_INVALID, "raw_type %d", raw_type);
+  if (pmode < 0 || pmode > 2 || (pmode == 1 && npol < 2))
+    return fail(ctx, PPF_ERR_INVALID, "pmode %d with npol %d", pmode, npol);
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  const int npo = pmode ? 1 : npol;
+  const size_t total = (size_t)nsub * npo * nchan * nbin;
+  const dim3 g((unsigned)((total + 255) / 256));
+  return timed(ctx, PPF_K_UNPACK, [&] {
+    switch (raw_type) {
+      case 1:
+        hipLaunchKernelGGL(k_unpack<uint8_t>, g, dim3(256), 0, ctx->stream,
+                           static_cast<const uint8_t*>(raw), scl, offs, nsub, npol, nchan, nbin,
+                           pmode, out);
+        break;
+      case 2:
+        hipLaunchKernelGGL(k_unpack<int16_t>, g, dim3(256), 0, ctx->stream,
+                           static_cast<const int16_t*>(raw), scl, offs, nsub, npol, nchan, nbin,
+                           pmode, out);
+        break;
+      default:
+        hipLaunchKernelGGL(k_unpack<float>, g, dim3(256), 0, ctx->stream,
+                           static_cast<const float*>(raw), scl, offs, nsub, npol, nchan, nbin,
+                           pmode, out);
+    }
+  });
+}
+
 int ppf_resid_chi2_rows(ppf_ctx* ctx, int32_t nrow, int32_t nbin, const double* data,
                         const double* phase, const double* model, const int32_t* model_row,
                         const double* scale, const double* tau, const double* errs,

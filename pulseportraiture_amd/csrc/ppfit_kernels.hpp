@@ -422,6 +422,9 @@ __global__ void k_accum_reduce(const double2* partial, double2* accum, int nspli
 template <int LOGN> __global__ void k_resid_chi2(ResidArgs a, const double2* tw);
 __global__ void k_vpow(double2* vp, int N, int rows);
 __global__ void k_gauss_port(GaussArgs g, const double* freqs, double* out);
+template <typename T>
+__global__ void k_unpack(const T* raw, const double* scl, const double* offs, int nsub, int npol,
+                         int nchan, int nbin, int pmode, double* out);
 __global__ void k_scat_taus(const double* freqs, int n, double tau, double alpha, double nu_ref,
                             double* out);
 __global__ void k_guess(FitArgs a);

@@ -134,4 +134,43 @@ __global__ void k_scat_taus(const double* __restrict__ freqs, int n, double tau,
   if (i < n) out[i] = tau * pow(freqs[i] / nu_ref, alpha);
 }
 
+// ---------------------------------------------------------------------------
+// PSRFITS unpacking (load_data's Archive_load + pscrunch, pplib.py:2670-2732):
+// out[s][q][n][j] = sum over the polarisations q takes of
+//   raw[s][p][n][j] * scl[s][p][n] + offs[s][p][n]
+// with pmode 0: every polarisation kept (q = p), 1: q = 0 takes p = 0 and 1
+// (AA + BB, coherence or 2-pol data), 2: q = 0 takes p = 0 (Stokes I).
+// One thread per output sample (raw read once, coalesced along the bins).
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ void k_unpack(const T* __restrict__ raw, const double* __restrict__ scl,
+                         const double* __restrict__ offs, int nsub, int npol, int nchan,
+                         int nbin, int pmode, double* __restrict__ out) {
+  const int npo = pmode ? 1 : npol;
+  const size_t total = (size_t)nsub * npo * nchan * nbin;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int j = (int)(i % nbin);
+  size_t r = i / nbin;
+  const int n = (int)(r % nchan);
+  r /= nchan;
+  const int q = (int)(r % npo);
+  const size_t s = r / npo;
+  auto val = [&](int p) {
+    const size_t m = (s * npol + p) * nchan + n;
+    return fma((double)raw[m * nbin + j], scl[m], offs[m]);
+  };
+  double v;
+  if (pmode == 1) v = val(0) + val(1);
+  else v = val(pmode == 2 ? 0 : q);
+  out[i] = v;
+}
+
+template __global__ void k_unpack<uint8_t>(const uint8_t*, const double*, const double*, int, int,
+                                           int, int, int, double*);
+template __global__ void k_unpack<int16_t>(const int16_t*, const double*, const double*, int, int,
+                                           int, int, int, double*);
+template __global__ void k_unpack<float>(const float*, const double*, const double*, int, int, int,
+                                         int, int, double*);
+
 }  // namespace ppf

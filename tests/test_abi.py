@@ -40,3 +40,15 @@ def test_no_device_fails_loudly():
     from pulseportraiture_amd.engine import Engine, PPFitError
     with pytest.raises(PPFitError):
         Engine(0)
+
+
+def test_ppfits_library_exports_header():
+    """libppfits.so (include/ppfits.h, host PSRFITS reader) exports every entry point."""
+    from pulseportraiture_amd import build, psrfits
+    build.build_fits()
+    txt = open(os.path.join(ROOT, "include", "ppfits.h")).read()
+    syms = sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(ppfits_\w+)\s*\(", txt, re.M)))
+    assert len(syms) == 7
+    lib = psrfits.load_library()
+    for s in syms:
+        assert hasattr(lib, s), s
