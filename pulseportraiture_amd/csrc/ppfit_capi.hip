@@ -350,7 +350,7 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
 
   // per-subint workspace layout
   const size_t bX = (size_t)nchan * NHP * sizeof(double2);
-  const size_t bT = taylor ? (size_t)2 * nchan * (kMT * sizeof(double2) + sizeof(int)) : 0;
+  const size_t bT = taylor ? (size_t)2 * nchan * kMT * sizeof(double2) : 0;
   const size_t bR = (size_t)NHP * sizeof(double2);
   const size_t bC = (size_t)nchan * sizeof(double);
   const size_t bAcc = (size_t)2 * nchan * 10 * sizeof(double);
@@ -397,7 +397,7 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   sa.dsum = reinterpret_cast<double*>(base + offDs);
   sa.tw = tw;
 
-  FitArgs fa;
+  FitArgs fa{};
   fa.nchan = nchan;
   fa.nbin = nbin;
   fa.NH = NH;
@@ -433,8 +433,6 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   fa.acc = reinterpret_cast<double*>(base + offAcc);
   fa.wsc = reinterpret_cast<double*>(base + offW);
   fa.T = taylor ? reinterpret_cast<double2*>(base + offT) : nullptr;
-  fa.Tcnt = taylor ? reinterpret_cast<int*>(base + offT + cs * 2 * nchan * kMT * sizeof(double2))
-                   : nullptr;
   fa.tw = tw;
   fa.vpow = nullptr;
   if (taylor)
@@ -460,6 +458,10 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   fa.o_hess = o->hess;
 
   const size_t lds_meta = align256((size_t)nchan * (5 * sizeof(double) + sizeof(int)));
+  // k_fit_taylor keeps T slot 0 in LDS when it fits (kTaylorLds)
+  const size_t tl_bytes = (size_t)nchan * kMT * sizeof(double2);
+  fa.tlds = (taylor && tl_bytes <= kTaylorLds) ? (int)lds_meta : 0;
+  const size_t lds_taylor = lds_meta + (fa.tlds ? tl_bytes : 0);
   // trust-ncg scattering fits: every evaluation split over blocks of >= 64
   // fitted channels (k_scat_sweep / k_scat_step)
   static const bool split_on = [] {
@@ -540,7 +542,7 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
           }))
         return r;
       if (int r = timed(ctx, PPF_K_FIT_TAYLOR, [&] {
-            hipLaunchKernelGGL(k_fit_taylor, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
+            hipLaunchKernelGGL(k_fit_taylor, dim3(nc), dim3(kBlock), lds_taylor, ctx->stream, fa);
           }))
         return r;
     }

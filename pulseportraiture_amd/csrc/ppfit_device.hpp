@@ -112,6 +112,18 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+// wave_sum of a value held only by the lanes with (lane & 7) == 0 (zero on
+// the rest), without the group8_sum stage that only adds those zeros: row_shr
+// 8 pairs the row's two holders, then the row and half-wave swaps.  Every
+// addition meets the same two operands as in wave_sum (in commuted order),
+// so the result is bitwise wave_sum's; it is valid on lanes (lane & 15) == 8.
+__device__ __forceinline__ double chan8_sum(double v) {
+  v += dpp_mov<0x118>(v);  // row_shr:8 (lanes 0-7 of a row receive 0)
+  v += swap_rows<16>(v);
+  v += swap_rows<32>(v);
+  return v;
+}
+
 // Max over the wave; every lane gets it.
 __device__ __forceinline__ double wave_max(double v) {
   v = fmax(v, dpp_mov<0xB1>(v));

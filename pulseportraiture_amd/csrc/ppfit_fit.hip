@@ -379,10 +379,10 @@ __constant__ double c_inv_fact[kMT] = {
 
 struct TaylorSrc {
   const double2* T;    // this subint's moment rows for one centre: [nchan][kMT], or null (exact)
-  const int* cnt;      // [nchan] moments stored per row
   const double* xc;    // centre params
   const double* refc;  // centre reference frequencies
   bool same = false;   // evaluation refs == refc: offsets from Meta d1/d2
+  const double* ifact = nullptr;  // LDS copy of c_inv_fact, or null (constant memory)
 };
 
 // offset from the centre for evaluation refs == centre refs:
@@ -400,9 +400,11 @@ __device__ __forceinline__ double taylor_delta(const double* prm, const double* 
   return d - rint(d);
 }
 
-__device__ __forceinline__ void taylor_cells(const double2* __restrict__ Tn, int cnt, int h,
-                                             double d, double Ks, double* acc) {
-  const int mterm = cnt - 2;  // terms of the series (T up to index cnt - 1)
+__device__ __forceinline__ void taylor_cells(const double2* __restrict__ Tn, int h, double d,
+                                             double Ks, const double* ifact, double* acc) {
+  // 1/m! by lane-varying m: from LDS when the caller staged it (a constant-
+  // memory gather costs a memory round trip per call)
+  const double* fz = ifact ? ifact : c_inv_fact;
   const double y = kTwoPi * Ks * d;
   double yh = 1.0;
   for (int i = 0; i < h; ++i) yh *= y;
@@ -412,8 +414,8 @@ __device__ __forceinline__ void taylor_cells(const double2* __restrict__ Tn, int
 #pragma unroll
   for (int q = 0; q < (kMTerm + 7) / 8; ++q) {
     const int m = h + 8 * q;
-    if (m < mterm) {
-      const double cf = ym * c_inv_fact[m];
+    if (m < kMTerm) {  // T up to index kMTerm + 1 = kMT - 1
+      const double cf = ym * fz[m];
       const double2 t0 = Tn[m], t1 = Tn[m + 1], t2 = Tn[m + 2];
       S0 = cmk(fma(cf, t0.x, S0.x), fma(cf, t0.y, S0.y));
       S1 = cmk(fma(cf, t1.x, S1.x), fma(cf, t1.y, S1.y));
@@ -454,6 +456,13 @@ __device__ double taylor_reach(const Meta& m, const double* prm, const double* r
   return kTwoPi * Ks * r;
 }
 
+__device__ __forceinline__ int flag_mask(const FitArgs& a) {
+  int fm = 0;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) fm |= a.flags[i] ? 1 << i : 0;
+  return fm;
+}
+
 // Solver sweep of a phase-family fit from Taylor moments (refs = nu_fit, so
 // d phi_n / d(DM, GM) are Meta's d1, d2).  With tau = 0, S_n = p_n / errs^2
 // does not depend on the parameters and every term of pptoaslib.py:525-643
@@ -472,54 +481,69 @@ __device__ void sweep_taylor0(const FitArgs& a, const Meta& m, const double* prm
 #pragma unroll
   for (int i = 0; i < 10; ++i) t[i] = 0.0;
   const int ngroups = (m.nok + 7) >> 3;
-  for (int gi = w; gi < ngroups; gi += kWaves) {
-    const int j = gi * 8 + g8;
-    const bool valid = j < m.nok;
-    const int jj = valid ? j : m.nok - 1;
-    const int n = m.chan[jj];
-    const double d1 = m.d1[jj], d2 = m.d2[jj];
-    double acc[NACC];
-    taylor_cells(ts.T + (size_t)n * kMT, ts.cnt[n], h, taylor_delta_lin(prm, ts.xc, d1, d2), Ks,
-                 acc);
-    const double s0 = group8_sum(acc[0]), s1 = group8_sum(acc[1]), s2 = group8_sum(acc[2]);
-    if (h == 0 && valid) {
-      double* dst = acc_slot + (size_t)j * NACC;
-      dst[0] = s0;
-      dst[1] = s1;
-      dst[2] = s2;
-      const double iw2 = m.iw2[j];
-      const double C = s0 * iw2, C1 = -kTwoPi * s1 * iw2, C2 = -kFourPi2 * s2 * iw2;
-      const double iS = 1.0 / (m.pn[j] * iw2);
-      const double gc = -2.0 * C * C1 * iS;
-      const double hc = -2.0 * (C * C2 + C1 * C1) * iS;
-      t[0] -= C * C * iS;
-      t[1] += gc;
-      t[2] = fma(gc, d1, t[2]);
-      t[3] = fma(gc, d2, t[3]);
-      t[4] += hc;
-      t[5] = fma(hc, d1, t[5]);
-      t[6] = fma(hc, d2, t[6]);
-      t[7] = fma(hc * d1, d1, t[7]);
-      t[8] = fma(hc * d1, d2, t[8]);
-      t[9] = fma(hc * d2, d2, t[9]);
+  // a wave's groups two at a time (both series in flight), accumulated in
+  // group order
+  for (int gi = w; gi < ngroups; gi += 2 * kWaves) {
+    double sg[2][3];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int j = (gi + u * kWaves) * 8 + g8;
+      const int jj = j < m.nok ? j : m.nok - 1;
+      double acc[NACC];
+      taylor_cells(ts.T + (size_t)m.chan[jj] * kMT, h,
+                   taylor_delta_lin(prm, ts.xc, m.d1[jj], m.d2[jj]), Ks, ts.ifact, acc);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) sg[u][i] = group8_sum(acc[i]);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int j = (gi + u * kWaves) * 8 + g8;
+      const bool valid = j < m.nok;
+      const double s0 = sg[u][0], s1 = sg[u][1], s2 = sg[u][2];
+      if (h == 0 && valid) {
+        const double d1 = m.d1[j], d2 = m.d2[j];
+        double* dst = acc_slot + (size_t)j * NACC;
+        dst[0] = s0;
+        dst[1] = s1;
+        dst[2] = s2;
+        const double iw2 = m.iw2[j];
+        const double C = s0 * iw2, C1 = -kTwoPi * s1 * iw2, C2 = -kFourPi2 * s2 * iw2;
+        const double iS = 1.0 / (m.pn[j] * iw2);
+        const double gc = -2.0 * C * C1 * iS;
+        const double hc = -2.0 * (C * C2 + C1 * C1) * iS;
+        t[0] -= C * C * iS;
+        t[1] += gc;
+        t[2] = fma(gc, d1, t[2]);
+        t[3] = fma(gc, d2, t[3]);
+        t[4] += hc;
+        t[5] = fma(hc, d1, t[5]);
+        t[6] = fma(hc, d2, t[6]);
+        t[7] = fma(hc * d1, d1, t[7]);
+        t[8] = fma(hc * d1, d2, t[8]);
+        t[9] = fma(hc * d2, d2, t[9]);
+      }
     }
   }
+  // only the channel lanes (h == 0) hold terms
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
-    const double v = wave_sum(t[i]);
-    if (lane == 0) red[w][i] = v;
+    const double v = chan8_sum(t[i]);
+    if (lane == 8) red[w][i] = v;
   }
   __syncthreads();
   if (tid < 21) {
     // out[0] f, out[1..5] g, out[6 + p] H pair p: (0,0) 0, (0,1) 1, (0,2) 2,
     // (1,1) 5, (1,2) 6, (2,2) 9; tau/alpha entries are 0
+    // fit flags as a bit mask read with constant indices (scalar loads): a
+    // lane-indexed a.flags[] would be a vector load from kernarg memory
+    const int fm = flag_mask(a);
     int src = -1;
     bool on = true;
     if (tid == 0) src = 0;
-    else if (tid < 4) { src = tid; on = a.flags[tid - 1]; }
+    else if (tid < 4) { src = tid; on = (fm >> (tid - 1)) & 1; }
     else if (tid >= 6) {
       const int p = tid - 6, pi = pair_i(p), pj = pair_j(p);
-      if (pj < 3) { src = 4 + (pi == 0 ? pj : 1 + pi + pj); on = a.flags[pi] && a.flags[pj]; }
+      if (pj < 3) { src = 4 + (pi == 0 ? pj : 1 + pi + pj); on = (fm >> pi) & (fm >> pj) & 1; }
     }
     double v = 0.0;
     if (src >= 0 && on)
@@ -577,7 +601,7 @@ __device__ void sweep(const FitArgs& a, const Meta& m, int c, int s, const doubl
     if (!SCAT && ts.T) {
       const double dl = ts.same ? taylor_delta_lin(prm, ts.xc, m.d1[jj], m.d2[jj])
                                 : taylor_delta(prm, refs, ts, fr, P);
-      taylor_cells(ts.T + (size_t)n * kMT, ts.cnt[n], h, dl, 0.5 * (double)a.nbin, acc);
+      taylor_cells(ts.T + (size_t)n * kMT, h, dl, 0.5 * (double)a.nbin, ts.ifact, acc);
     } else if (!scat) {
       const double phif = phase_frac(prm, fr, refs, P);
       const double2* Xr = a.X + ((size_t)c * a.nchan + n) * a.NHP;
@@ -1498,6 +1522,7 @@ struct PostShared {
   double out[48];
   double red[kWaves][48];
   double Xinv[25];
+  double ifact[kMT];  // c_inv_fact for the Taylor sweep
   int ifit[5];
   int nfit, nok, bad;
   double fmean, Sd;
@@ -1635,17 +1660,17 @@ __device__ void post_subint(const FitArgs& a, int c, int s, unsigned char* dyn, 
   TaylorSrc ts{};
   if (!SCAT && st.taylor) {
     const double Ks = 0.5 * (double)a.nbin;
+    if (tid < kMT) sh.ifact[tid] = c_inv_fact[tid];  // published by taylor_reach's barriers
     int best = st.xslot;
     double by = INFINITY;
     for (int q = 0; q < 2; ++q) {
       if (!(st.mvalid & (1 << q))) continue;
-      const TaylorSrc tq{a.T + ((size_t)c * 2 + q) * nchan * kMT,
-                         a.Tcnt + ((size_t)c * 2 + q) * nchan, st.xc[q], st.refs};
+      const TaylorSrc tq{a.T + ((size_t)c * 2 + q) * nchan * kMT, st.xc[q], st.refs};
       const double y = taylor_reach(m, sh.prm, sh.nu, tq, P, Ks, sh.red[0]);
       if (y < by) { by = y; best = q; }
     }
-    ts = TaylorSrc{a.T + ((size_t)c * 2 + best) * nchan * kMT,
-                   a.Tcnt + ((size_t)c * 2 + best) * nchan, st.xc[best], st.refs};
+    ts = TaylorSrc{a.T + ((size_t)c * 2 + best) * nchan * kMT, st.xc[best], st.refs, false,
+                   sh.ifact};
   }
   mark(18);
   sweep<1, SCAT>(a, m, c, s, sh.prm, sh.nu, P, nullptr, sh.out, sh.red, ts, sh.lrow);

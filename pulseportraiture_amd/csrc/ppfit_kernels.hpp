@@ -49,6 +49,9 @@ constexpr int kMT = 32;
 // (k <= N plus the zero-padded tail of the last block of steps)
 __host__ __device__ constexpr int kVpowRows(int N) { return N + 1 + 4 * 64; }
 constexpr int kMTerm = kMT - 2;
+// largest LDS copy of one T slot k_fit_taylor keeps (48 KB: nchan <= 96), so
+// that two of its blocks (the register limit) still fit a CU's 160 KB of LDS
+constexpr size_t kTaylorLds = 48 * 1024;
 constexpr double kTaylorY = 3.0;
 
 // Per-subint solver state handed from k_guess -> k_solve -> k_post (global).
@@ -93,7 +96,8 @@ struct FitArgs {
   const double* guess_tau;   // [nsub] or null
   SolveState* st;            // chunk [c]
   double2* T;                // chunk [c][2][nchan][kMT] Taylor moments
-  int* Tcnt;                 // chunk [c][2][nchan] moments stored per row
+  int tlds;                  // k_fit_taylor: byte offset of its LDS copy of T slot 0 in
+                             // dynamic LDS (after the Meta arrays), 0 = read T from HBM
   const double2* tw;         // rfft twiddles e^{-2 pi i m / nbin}
   const double2* vpow;       // [kVpowRows(N)][16] (v^col, v^(16+col)), v = k / N
   const double2* Mmean;      // [nmodel][NHP] mean template spectrum or null

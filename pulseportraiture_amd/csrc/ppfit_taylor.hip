@@ -178,7 +178,6 @@ __device__ __forceinline__ void moment_tile16(const FitArgs& a, int c, int slot,
       Tn[kk + 4 * r] = cmk(d0[r], g0[r]);
       Tn[16 + kk + 4 * r] = cmk(d1[r], g1[r]);
     }
-    if (kk == 0) a.Tcnt[((size_t)c * 2 + slot) * a.nchan + n] = kMT;
   }
 }
 
@@ -240,7 +239,6 @@ __device__ __forceinline__ void moment_tile8(const FitArgs& a, int c, int slot, 
       Tn[2 * (kk + 4 * r) + part] = d0[r];
       Tn[2 * (16 + kk + 4 * r) + part] = d1[r];
     }
-    if (kk == 0 && part == 0) a.Tcnt[((size_t)c * 2 + slot) * a.nchan + n] = kMT;
   }
 }
 
@@ -264,7 +262,7 @@ __device__ void moments_from_X(const FitArgs& a, const Meta& m, int c, int s, in
 // (masked channels idle in their lane).
 // ---------------------------------------------------------------------------
 template <int U>
-__global__ __launch_bounds__(kBlock) void k_moments(FitArgs a) {
+__global__ __launch_bounds__(kBlock, 3) void k_moments(FitArgs a) {
   const int c = blockIdx.x, s = a.sub0 + c;
   if (!fused_taylor(a, s)) return;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -292,36 +290,49 @@ template __global__ void k_moments<8>(FitArgs);
 // ---------------------------------------------------------------------------
 struct TaylorShared {
   double x[5], xp[5];
+  double xc[2][5];  // the two centres (st.xc), read by every sweep
   double out[48];
   double red[kWaves][48];
-  int done, nok, slot, tslot;
+  double ifact[kMT];  // c_inv_fact for taylor_cells
+  int done, nok, slot, tslot, q, mvalid;
 };
 
-__device__ __forceinline__ int pick_centre(const FitArgs& a, const Meta& m, const SolveState& st,
-                                           int c, const double* prm, const double* refs, double P,
-                                           double* red, TaylorSrc& ts) {
-  const double Ks = 0.5 * (double)a.nbin;
-  int best = -1;
-  double by = INFINITY;
-  for (int q = 0; q < 2; ++q) {
-    if (!(st.mvalid & (1 << q))) continue;
-    const TaylorSrc tq{a.T + ((size_t)c * 2 + q) * a.nchan * kMT,
-                       a.Tcnt + ((size_t)c * 2 + q) * a.nchan, st.xc[q], st.refs, true};
-    const double y = taylor_reach(m, prm, refs, tq, P, Ks, red);
-    if (y <= kTaylorY && y < by) { by = y; best = q; ts = tq; }
+// T slot 0 of subint c into the kernel's LDS copy (all threads; the caller
+// syncs): nchan * kMT entries, kU loads in flight per thread.
+__device__ __forceinline__ void stage_T0(const FitArgs& a, int c, double2* tl) {
+  const double2* __restrict__ src = a.T + (size_t)c * 2 * a.nchan * kMT;
+  const int n = a.nchan * kMT;
+  constexpr int kU = 8;
+  for (int i0 = 0; i0 < n; i0 += kBlock * kU) {
+    double2 v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int i = i0 + u * kBlock + (int)threadIdx.x;
+      v[u] = i < n ? src[i] : cmk(0.0, 0.0);
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int i = i0 + u * kBlock + (int)threadIdx.x;
+      if (i < n) tl[i] = v[u];
+    }
   }
-  return best;
 }
 
-union FitShared {
-  GuessShared gs;
-  TaylorShared ts;
-  PostShared ps;
-};
+// taylor_reach for one wave (every lane gets it): the largest |y_n| over the
+// fitted channels for evaluating (p0, p1, p2) from centre xc, refs = nu_fit.
+__device__ __forceinline__ double wave_reach(const Meta& m, double p0, double p1, double p2,
+                                             const double* xc, double Ks) {
+  const double prm[3] = {p0, p1, p2};
+  double mx = 0.0;
+  for (int j = (int)threadIdx.x & 63; j < m.nok; j += 64)
+    mx = fmax(mx, fabs(taylor_delta_lin(prm, xc, m.d1[j], m.d2[j])));
+  return kTwoPi * Ks * wave_max(mx);
+}
 
-__global__ __launch_bounds__(kBlock) void k_fit_taylor(FitArgs a) {
+
+__global__ __launch_bounds__(kBlock, 3) void k_fit_taylor(FitArgs a) {
   extern __shared__ __align__(16) unsigned char dyn[];
-  __shared__ FitShared u;
+  __shared__ TaylorShared sh;
   __shared__ double refs[3];
   const int c = blockIdx.x, s = a.sub0 + c, tid = threadIdx.x;
   const int lane = tid & 63;
@@ -340,15 +351,22 @@ __global__ __launch_bounds__(kBlock) void k_fit_taylor(FitArgs a) {
   };
   unsigned char* dmeta = dyn;
   SolveState& st = a.st[c];
-  TaylorShared& sh = u.ts;
+  // T slot 0 (k_moments) read once into LDS: every sweep about centre 0 then
+  // reads LDS instead of HBM.  load_meta's barrier publishes it.
+  double2* tl = a.tlds ? reinterpret_cast<double2*>(dyn + a.tlds) : nullptr;
+  if (tl) stage_T0(a, c, tl);
   const Meta m = load_meta(a, c, s, dmeta, &sh.nok);
   const double P = a.P[s];
+  const double Ks = 0.5 * (double)a.nbin;
   if (tid < 5) sh.x[tid] = st.x[tid];
+  if (tid < 5) sh.xc[0][tid] = st.xc[0][tid];
   if (tid < 3) refs[tid] = st.refs[tid];
+  if (tid < kMT) sh.ifact[tid] = c_inv_fact[tid];
   if (tid == 0) {
     sh.done = (m.nok == 0);
     sh.slot = 0;
     sh.tslot = 0;
+    sh.mvalid = 1;
     st.mvalid = 1;  // slot 0: k_moments, about st.xc[0]
   }
   __syncthreads();
@@ -368,29 +386,58 @@ __global__ __launch_bounds__(kBlock) void k_fit_taylor(FitArgs a) {
       if (lane == pair_j(p)) HH[pair_i(p)] = v;
     }
   };
-  // a centre that covers p: a stored one, else p itself (one more X pass)
-  auto centre_for = [&](const double* p, TaylorSrc& ts) -> int {
-    int q = pick_centre(a, m, st, c, p, refs, P, sh.red[0], ts);
-    if (q >= 0) return q;
+  // the stored centre nearest p within reach (taylor_reach <= kTaylorY, the
+  // first of equals), or -1; wave 0 only, no barrier
+  auto pick = [&](double p0, double p1, double p2) -> int {
+    int best = -1;
+    double by = INFINITY;
+    for (int q = 0; q < 2; ++q) {
+      if (!(sh.mvalid & (1 << q))) continue;
+      const double y = wave_reach(m, p0, p1, p2, sh.xc[q], Ks);
+      if (y <= kTaylorY && y < by) { by = y; best = q; }
+    }
+    return best;
+  };
+  auto source = [&](int q) {
+    return TaylorSrc{(q == 0 && tl) ? tl : a.T + ((size_t)c * 2 + q) * a.nchan * kMT, sh.xc[q],
+                     refs, true, sh.ifact};
+  };
+  // no stored centre covers p: p itself becomes one (one more X pass)
+  auto recentre = [&](const double* p) -> int {
     const int wsl = sh.tslot ^ 1;
     ++nrc;
     if (tid == 0) {
       st.mvalid &= ~(1 << wsl);
+      sh.mvalid = st.mvalid;
       for (int i = 0; i < 5; ++i) st.xc[wsl][i] = p[i];
     }
+    if (tid < 5) sh.xc[wsl][tid] = p[tid];
     __syncthreads();
-    moments_from_X(a, m, c, s, wsl, st.xc[wsl], refs, P);
+    moments_from_X(a, m, c, s, wsl, sh.xc[wsl], refs, P);
     __syncthreads();
-    if (tid == 0) st.mvalid |= 1 << wsl;
+    if (wsl == 0 && tl) stage_T0(a, c, tl);
+    if (tid == 0) {
+      st.mvalid |= 1 << wsl;
+      sh.mvalid = st.mvalid;
+    }
     __syncthreads();
-    q = pick_centre(a, m, st, c, p, refs, P, sh.red[0], ts);
-    return q;  // p is that centre: |y| = 0
+    if (tid < 64) {
+      const int q = pick(p[0], p[1], p[2]);
+      if (lane == 0) sh.q = q;
+    }
+    __syncthreads();
+    return sh.q;  // p is that centre: |y| = 0
   };
   if (!sh.done) {
-    TaylorSrc ts{};
-    const int q = centre_for(sh.x, ts);
+    if (tid < 64) {
+      const int q0 = pick(sh.x[0], sh.x[1], sh.x[2]);
+      if (lane == 0) sh.q = q0;
+    }
+    __syncthreads();
+    int q = sh.q;
+    if (q < 0) q = recentre(sh.x);
     mark(2);
-    sweep<0, false>(a, m, c, s, sh.x, refs, P, acc0, sh.out, sh.red, ts);
+    sweep<0, false>(a, m, c, s, sh.x, refs, P, acc0, sh.out, sh.red, source(q));
     mark(3);
     if (tid < 64) {
       load_fgh(f, g, Hrow);
@@ -413,17 +460,20 @@ __global__ __launch_bounds__(kBlock) void k_fit_taylor(FitArgs a) {
       } else {
         pl = steihaug(f, g, Hrow, tr, hits);
         predv = model_val(f, g, Hrow, pl);
-        if (lane < 5) sh.xp[lane] = xl + pl;
+        const double pv = xl + pl;  // lane i < 5: component i of the proposal
+        if (lane < 5) sh.xp[lane] = pv;
+        const int qp = pick(__shfl(pv, 0), __shfl(pv, 1), __shfl(pv, 2));
+        if (lane == 0) sh.q = qp;
       }
     }
     __syncthreads();
     mark(4);
     if (sh.done) break;
-    TaylorSrc ts{};
-    const int q = centre_for(sh.xp, ts);
+    int q = sh.q;
+    if (q < 0) q = recentre(sh.xp);
     mark(2);
     double* sl = acc0 + (size_t)(sh.slot ^ 1) * a.nchan * NACC;
-    sweep<0, false>(a, m, c, s, sh.xp, refs, P, sl, sh.out, sh.red, ts);
+    sweep<0, false>(a, m, c, s, sh.xp, refs, P, sl, sh.out, sh.red, source(q));
     mark(3);
     if (tid < 64) {
       double fp, gp, Hp[5] = {0, 0, 0, 0, 0};

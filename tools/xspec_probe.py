@@ -1,4 +1,4 @@
-"""k_data_xspec time on the headline batch for the library named by PPF_LIB
+"""Kernel times on the headline batch for the library named by PPF_LIB
 (timing experiments: PPF_XP builds; results downstream of a crippled variant
 are meaningless, only the kernel clock is read)."""
 import os
@@ -28,5 +28,6 @@ eng.reset_kernel_times()
 for _ in range(3):
     eng.fit_batch(*args, nu_fit=nu, guess=True, guess_Ns=100)
 torch.cuda.synchronize()
-print(os.environ.get("PPF_LIB", "default"), "data_xspec ms %.3f" % (eng.kernel_time("data_xspec")[0] / 3),
-      "moments ms %.3f" % (eng.kernel_time("moments")[0] / 3))
+print(os.environ.get("PPF_LIB", "default"),
+      " ".join("%s %.3f" % (k, eng.kernel_time(k)[0] / 3)
+               for k in ["data_xspec", "guess", "moments", "fit_taylor", "post"]))
