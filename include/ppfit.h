@@ -87,6 +87,13 @@ const char* ppf_last_error(const ppf_ctx* ctx);
 /* hip stream (hipStream_t cast to void*); NULL selects the null stream */
 int ppf_set_stream(ppf_ctx* ctx, void* stream);
 int ppf_synchronize(ppf_ctx* ctx);
+/* Phase-family fits (trust-ncg, no tau/alpha) split each workspace chunk
+ * into `pieces` launches alternating between the context stream and a
+ * second internal queue, piece p's data pass ordered after piece p-1's, so
+ * one piece's latency-bound solver kernels overlap the next one's HBM-bound
+ * pass.  Results are bitwise those of pieces = 1.  0 = default (PPF_PIPE
+ * environment variable, else the library default); at most 64.            */
+int ppf_set_pipeline(ppf_ctx* ctx, int32_t pieces);
 /* Upper bound on workspace bytes the context may hold (default 32 GiB). */
 int ppf_set_workspace_limit(ppf_ctx* ctx, int64_t bytes);
 /* Per-kernel HIP-event timing on the context stream (off by default). */
@@ -223,6 +230,34 @@ int ppf_rotate_accumulate(ppf_ctx* ctx, int32_t nsub, int32_t nchan,
 int ppf_gaussian_portraits(ppf_ctx* ctx, int32_t nrow, int32_t nbin, int32_t ngauss,
                            const int32_t* code, const double* params, double nu_ref,
                            double alpha, const double* freqs, double* out);
+
+/* B-spline (PCA) template rows (gen_spline_portrait, pplib.py:932-956, as
+ * read_spline_model builds them, pplib.py:2961-2993): row r at freqs[r] is
+ * mean_prof + sum_e splev(freqs[r], (t, c[e], k), ext=0) eigvec[:, e]
+ * (FITPACK splev / fpbspl); neig == 0 tiles mean_prof.  When nbin_in !=
+ * nbin the rows are resampled as scipy.signal.resample (rfft branch) and
+ * rotated by 0.5 (1/nbin - 1/nbin_in) (rotate_portrait), both then powers
+ * of two in [64, 8192].  t HOST [nknot], c HOST [neig][ncoef] (ncoef >=
+ * nknot - k - 1), 1 <= k <= 5, neig <= 64; mean_prof [nbin_in], eigvec
+ * [nbin_in][neig], freqs [nrow], out [nrow][nbin] on the device.          */
+int ppf_spline_portraits(ppf_ctx* ctx, int32_t nrow, int32_t nbin_in, int32_t nbin, int32_t neig,
+                         const double* mean_prof, const double* eigvec, int32_t nknot, int32_t k,
+                         const double* t, const double* c, int32_t ncoef, const double* freqs,
+                         double* out);
+
+/* Instrumental-response convolution of template rows (get_TOAs with
+ * add_instrumental_response, pptoas.py:387-393): out[r] = irfft(R_r *
+ * rfft(in[r])) with R = instrumental_response_port_FT(nbin, freqs, DM, P,
+ * wids, irf_types) (pptoaslib.py:145-179): the product over nw responses
+ * (types HOST [nw]: 0 'rect' np.sinc(k wid), 1 'gauss' the normalised
+ * Gaussian FT of FWHM wid [rot] <= 0.1388; wids HOST [nw], > 0) and, when
+ * DM != 0, 'rect' of width 8.3e-6 chan_bw / (freqs[r] / 1e3)^3 / P (the
+ * reference's formula: DM only switches it on).  chan_bw is the caller's
+ * |freqs[1] - freqs[0]|.  in NULL: out receives R itself [nrow][nbin/2+1]. */
+int ppf_instrumental_response_rows(ppf_ctx* ctx, int32_t nrow, int32_t nbin, const double* in,
+                                   int32_t nw, const double* wids, const int32_t* types,
+                                   double DM, double chan_bw, double P, const double* freqs,
+                                   double* out);
 
 /* PSRFITS samples to physical values (PSRCHIVE's load + pscrunch in
  * load_data, pplib.py:2670-2732): raw [nsub][npol][nchan][nbin] of

@@ -709,3 +709,64 @@ def fit_subint_pptoas(portx, modelx, freqsx, weightsx, errs, SNRsx, P, DM_stored
     res.init = init
     res.nu_fit = nu_fit
     return res
+
+
+# ---------------------------------------------------------------------------
+# Template producers (SURVEY §8(f) #2 and pptoas.py:387-393)
+# ---------------------------------------------------------------------------
+def gen_spline_portrait(mean_prof, freqs, eigvec, tck, nbin=None):
+    """pplib.py:932-956: FITPACK splev (ext=0) of the B-spline curve at the
+    frequencies, projected back through the eigenvectors, plus the mean
+    profile; scipy.signal.resample and rotate_portrait (pplib.py:2428-2460)
+    when nbin differs from len(mean_prof)."""
+    import scipy.interpolate as si
+    import scipy.signal as ss
+    freqs = np.atleast_1d(freqs)
+    if not eigvec.shape[1]:
+        port = np.tile(mean_prof, len(freqs)).reshape(len(freqs), len(mean_prof))
+    else:
+        proj_port = np.array(si.splev(freqs, tck, der=0, ext=0)).T
+        port = np.dot(proj_port, eigvec.T) + mean_prof
+    if nbin is not None and len(mean_prof) != nbin:
+        shift = 0.5 * (nbin ** -1 - len(mean_prof) ** -1)
+        port = ss.resample(port, nbin, axis=1)
+        pFFT = np.fft.rfft(port, axis=1)
+        pFFT *= np.exp(np.arange(pFFT.shape[1]) * 2.0j * np.pi * shift)
+        port = np.fft.irfft(pFFT, axis=1)
+    return port
+
+
+def instrumental_response_FT(nbin, wid=0.0, irf_type="rect"):
+    """pptoaslib.py:112-143 (with gaussian_profile_FT, pptoaslib.py:14-50)."""
+    from scipy.special import erf
+    nharm = nbin // 2 + 1
+    if wid == 0.0:
+        return np.ones(nharm)
+    if irf_type == "rect":
+        return np.sinc(np.arange(nharm) * wid)
+    sigma = wid / (2 * np.sqrt(2 * np.log(2)))
+    amp = (2 * np.pi * sigma ** 2) ** 0.5
+    sigma = 1 / (sigma * 2 * np.pi)
+    harmind = np.arange(nharm)
+    a = sigma / ((1.0 / np.pi) * 2 ** 0.5)
+    b = harmind / (sigma * 2 ** 0.5)
+    gp = np.nan_to_num(np.exp(-b ** 2) * (erf(a - b * 1j) + erf(a + b * 1j)) / 2 * amp * nbin)
+    return gp / gp[0]
+
+
+def instrumental_response_port_FT(nbin, freqs, DM=0.0, P=1.0, wids=(), irf_types=()):
+    """pptoaslib.py:145-179: product of the responses; DM switches on a rect
+    smearing response of width 8.3e-6 chan_bw / (freq / 1e3)^3 / P."""
+    nharm = nbin // 2 + 1
+    nchan = len(freqs)
+    if DM == len(wids) == 0.0:
+        return np.ones([nchan, nharm])
+    R = np.ones([nchan, nharm], dtype=complex)
+    for wid, t in zip(wids, irf_types):
+        R *= np.tile(instrumental_response_FT(nbin, wid, t), nchan).reshape(nchan, nharm)
+    if DM:
+        chan_bw = abs(freqs[1] - freqs[0])
+        for ichan, freq in enumerate(freqs):
+            wid = 8.3e-6 * chan_bw / (freq / 1e3) ** 3 / P
+            R[ichan] *= instrumental_response_FT(nbin, wid, "rect")
+    return R

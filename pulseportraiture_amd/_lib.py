@@ -62,6 +62,7 @@ EXPORTS = {
     "ppf_last_error": ([ctypes.c_void_p], ctypes.c_char_p),
     "ppf_set_stream": ([ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
     "ppf_synchronize": ([ctypes.c_void_p], ctypes.c_int),
+    "ppf_set_pipeline": ([ctypes.c_void_p, ctypes.c_int32], ctypes.c_int),
     "ppf_set_workspace_limit": ([ctypes.c_void_p, ctypes.c_int64], ctypes.c_int),
     "ppf_set_timing": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
     "ppf_get_kernel_time": ([ctypes.c_void_p, ctypes.c_int,
@@ -94,6 +95,13 @@ EXPORTS = {
                                ctypes.c_int),
     "ppf_scatter_rotate_rows": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, _dp, _dp, _dp,
                                  _dp], ctypes.c_int),
+    "ppf_spline_portraits": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                              ctypes.c_int32, _dp, _dp, ctypes.c_int32, ctypes.c_int32, _dp, _dp,
+                              ctypes.c_int32, _dp, _dp], ctypes.c_int),
+    "ppf_instrumental_response_rows": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, _dp,
+                                        ctypes.c_int32, _dp, _dp, ctypes.c_double,
+                                        ctypes.c_double, ctypes.c_double, _dp, _dp],
+                                       ctypes.c_int),
     "ppf_synth_portraits": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
                              ctypes.c_int32, _dp, _dp, ctypes.c_double,
                              ctypes.c_uint64, ctypes.c_int64, _dp], ctypes.c_int),

@@ -43,7 +43,11 @@ struct ppf_ctx {
   Buffer mmean;   // mean template spectra (guess)
   Buffer ptime;   // k_fit_taylor phase clocks (ppf_phase_profile)
   Buffer spart;   // split scattering solve: block partials + running count
+  Buffer tmpl;    // template builders: knots / coefficients, rows and spectra
   int* active_h = nullptr;  // pinned host copy of the running count
+  hipStream_t stream2 = nullptr;        // second queue of the piece pipeline
+  int pipe = 0;                         // pieces per chunk (0: default)
+  std::vector<hipEvent_t> sync_events;  // ordering events (no timing)
   bool phase_prof = false;
   bool timing = false;
   std::vector<TimedLaunch> pending;
@@ -151,21 +155,48 @@ hipEvent_t ev_get(ppf_ctx* ctx) {
 
 // Launch helper: optional HIP-event bracket on the context stream.
 template <typename F>
-int timed(ppf_ctx* ctx, int kid, F&& launch) {
+int timed_on(ppf_ctx* ctx, int kid, hipStream_t st, F&& launch) {
   hipEvent_t a = nullptr, b = nullptr;
   if (ctx->timing) {
     a = ev_get(ctx);
     b = ev_get(ctx);
-    HIPCHK(ctx, hipEventRecord(a, ctx->stream));
+    HIPCHK(ctx, hipEventRecord(a, st));
   }
   launch();
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(ctx, PPF_ERR_DEVICE, "kernel %d launch: %s", kid, hipGetErrorString(e));
   if (ctx->timing) {
-    HIPCHK(ctx, hipEventRecord(b, ctx->stream));
+    HIPCHK(ctx, hipEventRecord(b, st));
     ctx->pending.push_back({kid, a, b});
   }
   return PPF_OK;
+}
+
+template <typename F>
+int timed(ppf_ctx* ctx, int kid, F&& launch) {
+  return timed_on(ctx, kid, ctx->stream, launch);
+}
+
+// i-th ordering event of the context (created on first use)
+int sync_event(ppf_ctx* ctx, size_t i, hipEvent_t* out) {
+  while (ctx->sync_events.size() <= i) {
+    hipEvent_t e;
+    HIPCHK(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ctx->sync_events.push_back(e);
+  }
+  *out = ctx->sync_events[i];
+  return PPF_OK;
+}
+
+// default pieces per chunk of the two-queue pipeline on the Taylor path
+// (PPF_PIPE overrides; 1 = one queue, the chunk as one launch per kernel)
+int pipe_default() {
+  static const int n = [] {
+    const char* e = getenv("PPF_PIPE");
+    const int v = e ? atoi(e) : 1;
+    return std::max(1, std::min(64, v));
+  }();
+  return n;
 }
 
 int resolve_timing(ppf_ctx* ctx) {
@@ -243,10 +274,16 @@ void ppf_ctx_destroy(ppf_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   for (auto& t : ctx->pending) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
   for (auto e : ctx->pool) (void)hipEventDestroy(e);
+  for (auto e : ctx->sync_events) (void)hipEventDestroy(e);
+  if (ctx->stream2) {
+    (void)hipStreamSynchronize(ctx->stream2);
+    (void)hipStreamDestroy(ctx->stream2);
+  }
   for (auto p : ctx->tw) if (p) (void)hipFree(p);
   for (auto p : ctx->vp) if (p) (void)hipFree(p);
   if (ctx->ptime.p) (void)hipFree(ctx->ptime.p);
   if (ctx->spart.p) (void)hipFree(ctx->spart.p);
+  if (ctx->tmpl.p) (void)hipFree(ctx->tmpl.p);
   if (ctx->active_h) (void)hipHostFree(ctx->active_h);
   if (ctx->ws.p) (void)hipFree(ctx->ws.p);
   if (ctx->mspec.p) (void)hipFree(ctx->mspec.p);
@@ -260,6 +297,12 @@ const char* ppf_last_error(const ppf_ctx* ctx) { return ctx ? ctx->err.c_str() :
 int ppf_set_stream(ppf_ctx* ctx, void* stream) {
   if (!ctx) return PPF_ERR_INVALID;
   ctx->stream = reinterpret_cast<hipStream_t>(stream);
+  return PPF_OK;
+}
+
+int ppf_set_pipeline(ppf_ctx* ctx, int32_t pieces) {
+  if (!ctx || pieces < 0 || pieces > 64) return PPF_ERR_INVALID;
+  ctx->pipe = pieces;
   return PPF_OK;
 }
 
@@ -477,6 +520,80 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
     if (!ctx->active_h) HIPCHK(ctx, hipHostMalloc(&ctx->active_h, sizeof(int)));
   }
   const size_t lds_guess = (size_t)NHP * sizeof(double2);
+  // Phase-family Taylor path, several pieces per chunk on two queues: piece
+  // p's data pass starts when piece p-1's has finished, so the latency-bound
+  // guess / fit / post-fit kernels of one piece run beside the HBM-bound
+  // data pass of the next.  Each piece owns its slice of the workspace.
+  const int pieces = ctx->pipe > 0 ? ctx->pipe : pipe_default();
+  const bool phase_family = !d->fit_flags[3] && !d->fit_flags[4];
+  if (taylor && !tnc && phase_family && pieces > 1) {
+    if (!ctx->stream2)
+      HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
+    hipEvent_t start, prev_x = nullptr;
+    if (int r = sync_event(ctx, 0, &start)) return r;
+    HIPCHK(ctx, hipEventRecord(start, ctx->stream));  // templates, tables, earlier calls
+    HIPCHK(ctx, hipStreamWaitEvent(ctx->stream2, start, 0));
+    size_t ev = 1;
+    for (int64_t s0 = 0; s0 < d->nsub; s0 += chunk) {
+      const int nc = (int)std::min<int64_t>(chunk, d->nsub - s0);
+      const int np = std::min(pieces, nc);
+      const int ps = (nc + np - 1) / np;
+      for (int p = 0; p * ps < nc; ++p) {
+        const int off = p * ps, n = std::min(ps, nc - off);
+        hipStream_t st = (p & 1) ? ctx->stream2 : ctx->stream;
+        SpecArgs sp = sa;
+        FitArgs fp = fa;
+        sp.sub0 = fp.sub0 = (int)s0 + off;
+        sp.X = sa.X + (size_t)off * nchan * NHP;
+        fp.X = sp.X;
+        sp.R = sa.R + (size_t)off * NHP;
+        fp.R = sp.R;
+        sp.sig = sa.sig + (size_t)off * nchan;
+        fp.sig = sp.sig;
+        sp.dsum = sa.dsum + (size_t)off * nchan;
+        fp.dsum = sp.dsum;
+        fp.st = fa.st + off;
+        fp.T = fa.T + (size_t)off * 2 * nchan * kMT;
+        fp.acc = fa.acc + (size_t)off * 2 * nchan * 10;
+        fp.wsc = fa.wsc + (size_t)off * nchan * 8;
+        if (prev_x) HIPCHK(ctx, hipStreamWaitEvent(st, prev_x, 0));
+        if (int r = timed_on(ctx, PPF_K_DATA_XSPEC, st, [&] {
+              LOGN_SWITCH(logN, hipLaunchKernelGGL(k_data_xspec<LG>, dim3(n),
+                                                   dim3(XspecCfg<LG>::WPB * 64),
+                                                   (size_t)nchan * sizeof(double2), st, sp));
+            }))
+          return r;
+        if (int r = sync_event(ctx, ev++, &prev_x)) return r;
+        HIPCHK(ctx, hipEventRecord(prev_x, st));
+        if (int r = timed_on(ctx, PPF_K_GUESS, st, [&] {
+              hipLaunchKernelGGL(k_guess, dim3(n), dim3(kBlock), d->guess ? lds_guess : 0, st, fp);
+            }))
+          return r;
+        if (int r = timed_on(ctx, PPF_K_MOMENTS, st, [&] {
+              const dim3 g(n, (nchan + 16 * kWaves - 1) / (16 * kWaves));
+              if (moments_u() == 4)
+                hipLaunchKernelGGL(k_moments<4>, g, dim3(kBlock), 0, st, fp);
+              else
+                hipLaunchKernelGGL(k_moments<8>, g, dim3(kBlock), 0, st, fp);
+            }))
+          return r;
+        if (int r = timed_on(ctx, PPF_K_FIT_TAYLOR, st, [&] {
+              hipLaunchKernelGGL(k_fit_taylor, dim3(n), dim3(kBlock), lds_taylor, st, fp);
+            }))
+          return r;
+        if (int r = timed_on(ctx, PPF_K_POST, st, [&] {
+              hipLaunchKernelGGL(k_post<false>, dim3(n), dim3(kBlock), lds_meta, st, fp);
+            }))
+          return r;
+      }
+    }
+    // join: the caller's stream sees every piece
+    hipEvent_t done;
+    if (int r = sync_event(ctx, ev++, &done)) return r;
+    HIPCHK(ctx, hipEventRecord(done, ctx->stream2));
+    HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, done, 0));
+    return PPF_OK;
+  }
   for (int64_t s0 = 0; s0 < d->nsub; s0 += chunk) {
     const int nc = (int)std::min<int64_t>(chunk, d->nsub - s0);
     sa.sub0 = (int)s0;
@@ -658,6 +775,135 @@ int ppf_scatter_rotate_rows(ppf_ctx* ctx, int32_t nrow, int32_t nbin, const doub
   return timed(ctx, PPF_K_ROTATE, [&] {
     LOGN_SWITCH(logN, hipLaunchKernelGGL(k_rotate_rows<LG>, dim3(nrow), dim3(kBlock), 0,
                                          ctx->stream, in, phase, tau, out, tw));
+  });
+}
+
+int ppf_spline_portraits(ppf_ctx* ctx, int32_t nrow, int32_t nbin_in, int32_t nbin, int32_t neig,
+                         const double* mean_prof, const double* eigvec, int32_t nknot, int32_t k,
+                         const double* t, const double* c, int32_t ncoef, const double* freqs,
+                         double* out) {
+  if (!ctx || !mean_prof || !freqs || !out || (neig > 0 && (!eigvec || !t || !c)))
+    return fail(ctx, PPF_ERR_INVALID, "null argument");
+  if (nrow <= 0) return PPF_OK;
+  if (neig < 0 || neig > kMaxEig)
+    return fail(ctx, PPF_ERR_UNSUPPORTED, "neig=%d: at most %d eigenvectors", neig, kMaxEig);
+  if (neig > 0) {
+    if (k < 1 || k > kMaxSplineK)
+      return fail(ctx, PPF_ERR_UNSUPPORTED, "spline degree k=%d: 1..%d", k, kMaxSplineK);
+    if (nknot < 2 * (k + 1) || ncoef < nknot - k - 1)
+      return fail(ctx, PPF_ERR_INVALID, "nknot=%d, ncoef=%d: need nknot >= 2(k+1), ncoef >= nknot-k-1",
+                  nknot, ncoef);
+  }
+  if (nbin_in <= 0) return fail(ctx, PPF_ERR_INVALID, "nbin_in=%d", nbin_in);
+  int logI = 0, logO = 0;
+  const bool resample = nbin_in != nbin;
+  if (resample) {
+    if (int r = check_nbin(ctx, nbin_in, &logI)) return r;
+    if (int r = check_nbin(ctx, nbin, &logO)) return r;
+  } else if (nbin <= 0) {
+    return fail(ctx, PPF_ERR_INVALID, "nbin=%d", nbin);
+  }
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  // device copies of the knots and coefficients, then (resampling) the rows
+  // at nbin_in and both spectra
+  const size_t ntc = neig > 0 ? (size_t)nknot + (size_t)neig * ncoef : 0;
+  const size_t nrows_in = resample ? (size_t)nrow * nbin_in : 0;
+  const size_t hin = (size_t)nbin_in / 2 + 1, hout = (size_t)nbin / 2 + 1;
+  const size_t nspec = resample ? (size_t)nrow * (hin + hout) * 2 : 0;
+  if (int r = ensure(ctx, ctx->tmpl, (ntc + nrows_in + nspec) * sizeof(double))) return r;
+  double* base = static_cast<double*>(ctx->tmpl.p);
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));  // tmpl may still feed an earlier launch
+  SplineArgs s;
+  s.nbin = nbin_in;
+  s.neig = neig;
+  s.n = nknot;
+  s.k = k;
+  s.ncoef = ncoef;
+  s.t = base;
+  s.c = base + nknot;
+  s.mean = mean_prof;
+  s.eigvec = eigvec;
+  if (neig > 0) {
+    HIPCHK(ctx, hipMemcpy(base, t, (size_t)nknot * sizeof(double), hipMemcpyHostToDevice));
+    HIPCHK(ctx, hipMemcpy(base + nknot, c, (size_t)neig * ncoef * sizeof(double),
+                          hipMemcpyHostToDevice));
+  }
+  double* rows = resample ? base + ntc : out;
+  if (int r = timed(ctx, PPF_K_MODEL_FFT, [&] {
+        hipLaunchKernelGGL(k_spline_rows, dim3(nrow), dim3(256), 0, ctx->stream, s, freqs, rows);
+      }))
+    return r;
+  if (!resample) return PPF_OK;
+  double2* X = reinterpret_cast<double2*>(base + ntc + nrows_in);
+  double2* Y = X + (size_t)nrow * hin;
+  const double2 *twi, *two;
+  if (int r = twiddles(ctx, nbin_in, &twi)) return r;
+  if (int r = twiddles(ctx, nbin, &two)) return r;
+  // ss.resample introduces a shift, undone by rotate_portrait (pplib.py:953-955)
+  const double shift = 0.5 * (1.0 / (double)nbin - 1.0 / (double)nbin_in);
+  const size_t ny = (size_t)nrow * hout;
+  return timed(ctx, PPF_K_MODEL_FFT, [&] {
+    LOGN_SWITCH(logI, hipLaunchKernelGGL(k_rfft_rows<LG>, dim3(nrow), dim3(kBlock), 0, ctx->stream,
+                                         rows, X, twi));
+    hipLaunchKernelGGL(k_resample_spec, dim3((unsigned)((ny + 255) / 256)), dim3(256), 0,
+                       ctx->stream, X, nbin_in, nbin, shift, nrow, Y);
+    LOGN_SWITCH(logO, hipLaunchKernelGGL(k_irfft_rows<LG>, dim3(nrow), dim3(kBlock), 0,
+                                         ctx->stream, Y, out, two));
+  });
+}
+
+int ppf_instrumental_response_rows(ppf_ctx* ctx, int32_t nrow, int32_t nbin, const double* in,
+                                   int32_t nw, const double* wids, const int32_t* types,
+                                   double DM, double chan_bw, double P, const double* freqs,
+                                   double* out) {
+  if (!ctx || !out || (nw > 0 && (!wids || !types)) || (DM != 0.0 && !freqs))
+    return fail(ctx, PPF_ERR_INVALID, "null argument");
+  if (nrow <= 0) return PPF_OK;
+  if (nw < 0 || nw > kMaxIrf)
+    return fail(ctx, PPF_ERR_UNSUPPORTED, "nw=%d: at most %d responses", nw, kMaxIrf);
+  IrArgs g;
+  g.nw = nw;
+  g.fwhm = 2.0 * std::sqrt(2.0 * std::log(2.0));
+  for (int w = 0; w < nw; ++w) {
+    if (types[w] != 0 && types[w] != 1)
+      return fail(ctx, PPF_ERR_INVALID, "irf type %d: 0 (rect) or 1 (gauss)", types[w]);
+    if (!(wids[w] > 0.0))
+      return fail(ctx, PPF_ERR_INVALID, "irf width %g: must be > 0", wids[w]);
+    if (types[w] == 1) {
+      // a = 1 / (2 sqrt 2 sigma_t) >= 6 keeps the dropped exp(-a^2) w(z) term below 2.4e-16
+      const double st = wids[w] / g.fwhm;
+      if (1.0 / (2.0 * M_SQRT2 * st) < 6.0)
+        return fail(ctx, PPF_ERR_UNSUPPORTED,
+                    "gauss irf FWHM %g rot: supported up to %.4f rot", wids[w],
+                    g.fwhm / (12.0 * M_SQRT2));
+    }
+    g.type[w] = types[w];
+    g.wid[w] = wids[w];
+  }
+  g.dm_wid_num = DM != 0.0 ? 8.3e-6 * chan_bw : 0.0;
+  g.P = P;
+  if (DM != 0.0 && !(P > 0.0)) return fail(ctx, PPF_ERR_INVALID, "P=%g", P);
+  int logN;
+  if (int r = check_nbin(ctx, nbin, &logN)) return r;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  const size_t nh = (size_t)nbin / 2 + 1, n = (size_t)nrow * nh;
+  const unsigned grid = (unsigned)((n + 255) / 256);
+  if (!in)  // the response table R [nrow][nharm] itself
+    return timed(ctx, PPF_K_MODEL_FFT, [&] {
+      hipLaunchKernelGGL(k_ir_spec, dim3(grid), dim3(256), 0, ctx->stream, nullptr, out, nrow,
+                         (int)nh, g, freqs);
+    });
+  if (int r = ensure(ctx, ctx->tmpl, n * sizeof(double2))) return r;
+  double2* X = static_cast<double2*>(ctx->tmpl.p);
+  const double2* tw;
+  if (int r = twiddles(ctx, nbin, &tw)) return r;
+  return timed(ctx, PPF_K_MODEL_FFT, [&] {
+    LOGN_SWITCH(logN, hipLaunchKernelGGL(k_rfft_rows<LG>, dim3(nrow), dim3(kBlock), 0, ctx->stream,
+                                         in, X, tw));
+    hipLaunchKernelGGL(k_ir_spec, dim3(grid), dim3(256), 0, ctx->stream, X, nullptr, nrow, (int)nh,
+                       g, freqs);
+    LOGN_SWITCH(logN, hipLaunchKernelGGL(k_irfft_rows<LG>, dim3(nrow), dim3(kBlock), 0,
+                                         ctx->stream, X, out, tw));
   });
 }
 

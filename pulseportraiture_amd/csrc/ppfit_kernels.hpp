@@ -387,6 +387,25 @@ struct GaussArgs {
   double params[2 + 6 * kMaxGauss];  // DC, TAU, then loc, dloc, wid, dwid, amp, damp
 };
 
+constexpr int kMaxSplineK = 5, kMaxEig = 64;
+struct SplineArgs {
+  int nbin, neig, n, k, ncoef;  // bins, eigenvectors, knots, degree, coefficients per dimension
+  const double* t;              // [n] knots
+  const double* c;              // [neig][ncoef] B-spline coefficients
+  const double* mean;           // [nbin] mean profile
+  const double* eigvec;         // [nbin][neig]
+};
+
+constexpr int kMaxIrf = 16;
+struct IrArgs {
+  int nw;                 // instrumental responses besides the DM smearing
+  int type[kMaxIrf];      // 0 rect, 1 gauss
+  double wid[kMaxIrf];    // [rot]
+  double fwhm;            // 2 sqrt(2 ln 2) as numpy forms it
+  double dm_wid_num;      // 8.3e-6 chan_bw (0: no DM smearing response)
+  double P;               // period [s]
+};
+
 struct ResidArgs {
   const double* data;      // [nrow][nbin]
   const double* phase;     // [nrow] or NULL

@@ -135,6 +135,135 @@ __global__ void k_scat_taus(const double* __restrict__ freqs, int n, double tau,
 }
 
 // ---------------------------------------------------------------------------
+// B-spline (PCA) template portraits, gen_spline_portrait (pplib.py:932-956)
+// as read_spline_model builds them (pplib.py:2961-2993): row r at
+// freqs[r] is mean_prof + sum_e splev(freqs[r], (t, c[e], k)) eigvec[:, e].
+// splev is FITPACK's (splev.f with ext = 0: the knot interval search, then
+// fpbspl.f's de Boor recurrence, every product and sum rounded as gfortran
+// does without FMA); the eigenvector contraction (np.dot, a BLAS dgemm
+// whose summation order is the library's) is a fused sum over e.
+// ---------------------------------------------------------------------------
+__device__ double fp_splev(const double* __restrict__ t, int n, int k,
+                           const double* __restrict__ c, double x) {
+  const int k1 = k + 1, nk1 = n - k1;
+  // splev.f labels 35/40: the largest 1-based l in [k1, nk1] with t(l) <= x
+  int l = k1;
+  while (l != nk1 && x >= t[l]) ++l;  // t(l + 1) is t[l]
+  double h[kMaxSplineK + 1], hh[kMaxSplineK];
+  h[0] = 1.0;
+#pragma unroll
+  for (int j = 1; j <= kMaxSplineK; ++j) {
+    if (j > k) break;
+#pragma unroll
+    for (int i = 0; i < kMaxSplineK; ++i)
+      if (i < j) hh[i] = h[i];
+    h[0] = 0.0;
+#pragma unroll
+    for (int i = 1; i <= kMaxSplineK; ++i) {
+      if (i > j) break;
+      const double tli = t[l + i - 1], tlj = t[l + i - j - 1];
+      if (tli == tlj) {
+        h[i] = 0.0;
+        continue;
+      }
+      const double f = hh[i - 1] / (tli - tlj);
+      h[i - 1] = __dadd_rn(h[i - 1], __dmul_rn(f, tli - x));
+      h[i] = __dmul_rn(f, x - tlj);
+    }
+  }
+  double sp = 0.0;
+  const int ll = l - k1;
+#pragma unroll
+  for (int j = 0; j <= kMaxSplineK; ++j)
+    if (j < k1) sp = __dadd_rn(sp, __dmul_rn(c[ll + j], h[j]));
+  return sp;
+}
+
+__global__ __launch_bounds__(256) void k_spline_rows(SplineArgs s, const double* __restrict__ freqs,
+                                                     double* __restrict__ out) {
+  __shared__ double proj[kMaxEig];
+  const int r = blockIdx.x;
+  if ((int)threadIdx.x < s.neig)
+    proj[threadIdx.x] = fp_splev(s.t, s.n, s.k, s.c + (size_t)threadIdx.x * s.ncoef, freqs[r]);
+  __syncthreads();
+  double* o = out + (size_t)r * s.nbin;
+  for (int j = threadIdx.x; j < s.nbin; j += blockDim.x) {
+    const double* ev = s.eigvec + (size_t)j * s.neig;
+    double d = 0.0;
+    for (int e = 0; e < s.neig; ++e) d = fma(proj[e], ev[e], d);
+    o[j] = s.neig ? d + s.mean[j] : s.mean[j];  // eigvec.shape[1] == 0: the tiled mean
+  }
+}
+
+// scipy.signal.resample (rfft branch) of rows from nin to nout bins followed
+// by rotate_portrait(port, shift) (pplib.py:951-955), formed on the
+// spectrum: Y_k = X_k for k < min(nin, nout) / 2 + 1, the shared Nyquist
+// term x2 (down) or x0.5 (up), times nout / nin and e^{2 pi i k shift}; the
+// Nyquist imaginary part is dropped first, as resample's irfft drops it.
+__global__ void k_resample_spec(const double2* __restrict__ X, int nin, int nout, double shift,
+                                int nrow, double2* __restrict__ Y) {
+  const int ho = nout / 2 + 1, hi = nin / 2 + 1;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)nrow * ho) return;
+  const int k = (int)(i % ho);
+  const size_t r = i / ho;
+  const int N = min(nin, nout);
+  double2 y = cmk(0.0, 0.0);
+  if (k < N / 2 + 1) y = X[r * hi + k];
+  if (k == N / 2) {
+    if (nout < nin) y = cscale(y, 2.0);
+    else if (nin < nout) y = cscale(y, 0.5);
+  }
+  if (k == nout / 2) y.y = 0.0;
+  y = cscale(y, (double)nout / (double)nin);
+  if (shift != 0.0) y = cmul(y, turn_phasor((double)k, shift));
+  Y[i] = y;
+}
+
+// ---------------------------------------------------------------------------
+// Instrumental response (pptoas.py:387-393): spec[r][k] *= R_r(k) with
+// R_r = prod_w instrumental_response_FT(nbin, wids[w], types[w]) times, for
+// DM != 0, the rect response of width 8.3e-6 chan_bw / (freq_r / 1e3)^3 / P
+// (instrumental_response_port_FT, pptoaslib.py:145-179).  rect: np.sinc(k wid)
+// = sin(pi x) / (pi x) with x = 0 -> 1; gauss: gaussian_profile_FT(nbin, 0,
+// wid, 1) / its k = 0 term (pptoaslib.py:14-50, 136-139) =
+// exp(-b^2) Re erf(a + i b) / erf(a), taken as exp(-b^2) / erf(a) -- exact
+// to exp(-a^2) <= 2.4e-16 absolute for the widths the host admits (a >= 6).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double np_sinc(double x) {
+  const double y = __dmul_rn(M_PI, x == 0.0 ? 1.0e-20 : x);
+  return sin(y) / y;
+}
+
+__device__ __forceinline__ double irf_value(int type, double k, double wid, double fwhm) {
+  if (type == 0) return np_sinc(__dmul_rn(k, wid));
+  // gaussian_profile_FT: sigma = wid / (2 sqrt(2 ln 2)); sigma *= 2 pi; sigma = 1 / sigma
+  double sigma = wid / fwhm;
+  sigma = __dmul_rn(sigma, 2.0 * M_PI);
+  sigma = 1.0 / sigma;
+  const double a = sigma / __dmul_rn(1.0 / M_PI, M_SQRT2);
+  const double b = k / __dmul_rn(sigma, M_SQRT2);
+  return exp(-__dmul_rn(b, b)) / erf(a);
+}
+
+__global__ void k_ir_spec(double2* __restrict__ spec, double* __restrict__ resp, int nrow,
+                          int nharm, IrArgs g, const double* __restrict__ freqs) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)nrow * nharm) return;
+  const int k = (int)(i % nharm);
+  const int r = (int)(i / nharm);
+  double R = 1.0;
+  for (int w = 0; w < g.nw; ++w) R = __dmul_rn(R, irf_value(g.type[w], (double)k, g.wid[w], g.fwhm));
+  if (g.dm_wid_num != 0.0) {
+    const double fr = freqs[r] / 1e3;
+    const double wid = g.dm_wid_num / pow(fr, 3.0) / g.P;
+    R = __dmul_rn(R, np_sinc(__dmul_rn((double)k, wid)));
+  }
+  if (resp) resp[i] = R;  // the response table itself
+  else spec[i] = cscale(spec[i], R);
+}
+
+// ---------------------------------------------------------------------------
 // PSRFITS unpacking (load_data's Archive_load + pscrunch, pplib.py:2670-2732):
 // out[s][q][n][j] = sum over the polarisations q takes of
 //   raw[s][p][n][j] * scl[s][p][n] + offs[s][p][n]

@@ -482,6 +482,21 @@ __global__ __launch_bounds__(kBlock) void k_irfft_rows(const double2* __restrict
   c2r_from_spectrum<LOGN>(buf, xs, tw, out + (size_t)r * 2 * N);
 }
 
+// spec[r][k] = rfft(in[r])[k], k in [0, N] (numpy rfft layout; nothing zeroed)
+template <int LOGN>
+__global__ __launch_bounds__(kBlock) void k_rfft_rows(const double* __restrict__ in,
+                                                      double2* __restrict__ spec,
+                                                      const double2* __restrict__ tw) {
+  constexpr int N = 1 << LOGN;
+  __shared__ double2 buf[N];
+  const int r = blockIdx.x;
+  load_row<LOGN>(buf, in + (size_t)r * 2 * N);
+  __syncthreads();
+  lds_fft<LOGN, false>(buf, tw);
+  for (int k = threadIdx.x; k <= N; k += kBlock)
+    spec[(size_t)r * (N + 1) + k] = rfft_post<LOGN>(buf, k, tw);
+}
+
 template <int LOGN>
 __global__ __launch_bounds__(kBlock) void k_noise_rows(const double* __restrict__ in,
                                                        double* __restrict__ out, int kc,
@@ -664,6 +679,7 @@ __global__ __launch_bounds__(kBlock) void k_resid_chi2(ResidArgs a, const double
                                             double*, const double2*);                        \
   template __global__ void k_resid_chi2<L>(ResidArgs, const double2*);                       \
   template __global__ void k_irfft_rows<L>(const double2*, double*, const double2*);        \
+  template __global__ void k_rfft_rows<L>(const double*, double2*, const double2*);         \
   template __global__ void k_noise_rows<L>(const double*, double*, int, const double2*);    \
   template __global__ void k_synth<L>(const double2*, const double*, double*, int, int,      \
                                       double, uint64_t, int64_t, const double2*);            \

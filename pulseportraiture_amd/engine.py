@@ -105,6 +105,15 @@ class Engine:
     def synchronize(self):
         self._chk(self.lib.ppf_synchronize(self.ctx))
 
+    def set_workspace_limit(self, nbytes):
+        """Device workspace cap per fit call (ppf_set_workspace_limit)."""
+        self._chk(self.lib.ppf_set_workspace_limit(self.ctx, int(nbytes)))
+
+    def set_pipeline(self, pieces):
+        """Pieces per chunk of the two-queue phase-family pipeline
+        (ppf_set_pipeline; 0 = library default)."""
+        self._chk(self.lib.ppf_set_pipeline(self.ctx, int(pieces)))
+
     def set_timing(self, on=True):
         self._chk(self.lib.ppf_set_timing(self.ctx, int(bool(on))))
 
@@ -355,6 +364,82 @@ class Engine:
             _ptr(out)))
         out._keep = (f,)
         return out.reshape(shape + (nbin,))
+
+    def spline_portraits(self, mean_prof, eigvec, tck, freqs, nbin=None):
+        """gen_spline_portrait (pplib.py:932-956) on the device for every row
+        of freqs ([..., nchan]): FITPACK splev of the projections, the
+        eigenvector sum plus mean_prof, and (nbin != len(mean_prof)) the
+        resample + rotate.  Returns a device tensor [..., nchan, nbin]."""
+        dev = self.device
+        f = _dev_f64(freqs, dev)
+        shape = tuple(f.shape)
+        f = f.reshape(-1).contiguous()
+        mean = _dev_f64(np.asarray(mean_prof, dtype=np.float64), dev)
+        nin = int(mean.numel())
+        ev = np.asarray(eigvec, dtype=np.float64).reshape(nin, -1)
+        neig = ev.shape[1]
+        nb = nin if nbin is None else int(nbin)
+        t, c, k = tck[0], tck[1], tck[2]
+        if neig:
+            t = np.ascontiguousarray(t, dtype=np.float64)
+            c = np.ascontiguousarray(np.asarray(c, dtype=np.float64).reshape(neig, -1))
+            tp, cp, nknot, ncoef = t.ctypes.data, c.ctypes.data, len(t), c.shape[1]
+        else:
+            tp = cp = None
+            nknot = ncoef = 0
+        evd = _dev_f64(ev, dev) if neig else mean
+        out = torch.empty((f.numel(), nb), dtype=torch.float64, device=dev)
+        self._chk(self.lib.ppf_spline_portraits(
+            self.ctx, f.numel(), nin, nb, neig, _ptr(mean), _ptr(evd), nknot, int(k), tp, cp,
+            ncoef, _ptr(f), _ptr(out)))
+        out._keep = (f, mean, evd)
+        return out.reshape(shape + (nb,))
+
+    def _irf_call(self, nrow, nbin, rows, f, fh, DM, P, wids, irf_types, chan_bw, out):
+        code = {"rect": 0, "gauss": 1}
+        types = []
+        for t in irf_types:
+            if t not in code:
+                raise ValueError("Unrecognized instrumental response function type '%s'." % t)
+            types.append(code[t])
+        wids = [float(w) for w in wids]
+        if len(wids) != len(types):
+            raise ValueError("wids and irf_types differ in length")
+        if chan_bw is None:  # pptoaslib.py:174
+            chan_bw = abs(fh[1] - fh[0]) if len(fh) > 1 else 0.0
+        nw = len(wids)
+        wa = (ctypes.c_double * max(nw, 1))(*wids)
+        ta = (ctypes.c_int32 * max(nw, 1))(*types)
+        self._chk(self.lib.ppf_instrumental_response_rows(
+            self.ctx, nrow, nbin, _ptr(rows), nw, ctypes.cast(wa, ctypes.c_void_p),
+            ctypes.cast(ta, ctypes.c_void_p), float(DM), float(chan_bw), float(P), _ptr(f),
+            _ptr(out)))
+
+    def instrumental_response_rows(self, rows, freqs, DM=0.0, P=1.0, wids=(), irf_types=(),
+                                   chan_bw=None):
+        """irfft(instrumental_response_port_FT * rfft(rows)) (pptoas.py:387-393)
+        for rows [nrow, nbin] at freqs [nrow]; chan_bw defaults to
+        |freqs[1] - freqs[0]| as pptoaslib.py:174 takes it."""
+        dev = self.device
+        fh = np.asarray(freqs, dtype=np.float64).reshape(-1)
+        f = _dev_f64(fh, dev)
+        r = _dev_f64(rows, dev)
+        r2 = r.reshape(-1, r.shape[-1]).contiguous()
+        out = torch.empty_like(r2)
+        self._irf_call(r2.shape[0], r2.shape[1], r2, f, fh, DM, P, wids, irf_types, chan_bw, out)
+        out._keep = (r2, f)
+        return out.reshape(r.shape)
+
+    def response_table(self, nbin, freqs, DM=0.0, P=1.0, wids=(), irf_types=(), chan_bw=None):
+        """instrumental_response_port_FT (pptoaslib.py:145-179) as a real
+        device tensor [nchan, nbin/2+1]."""
+        dev = self.device
+        fh = np.asarray(freqs, dtype=np.float64).reshape(-1)
+        f = _dev_f64(fh, dev)
+        out = torch.empty((len(fh), nbin // 2 + 1), dtype=torch.float64, device=dev)
+        self._irf_call(len(fh), nbin, None, f, fh, DM, P, wids, irf_types, chan_bw, out)
+        out._keep = f
+        return out
 
     def irfft_rows(self, spec, nbin):
         dev = self.device

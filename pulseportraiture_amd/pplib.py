@@ -6,6 +6,7 @@ signatures (pplib.py) and its host-side producers/consumers:
 Gaussian-component templates (read_model / gen_gaussian_portrait,
 pplib.py:752-1046, 2834-2959) and the .tim writer (pplib.py:3386-3509).
 """
+import pickle
 import sys
 import time
 
@@ -165,7 +166,9 @@ def read_model(modelfile, phases=None, freqs=None, P=None, quiet=False):
     name = code = None
     nu_ref = dc = tau = alpha = 0.0
     fit_dc = fit_tau = fit_alpha = 0
-    for line in open(modelfile).readlines():
+    with open(modelfile, "rb") as fh:  # a pickled spline model is not UTF-8 text
+        lines = fh.read().decode("latin-1").splitlines()
+    for line in lines:
         info = line.split()
         if not info:
             continue
@@ -187,6 +190,11 @@ def read_model(modelfile, phases=None, freqs=None, P=None, quiet=False):
                 comps.append(line)
         except IndexError:
             pass
+    if name is None or code is None:
+        # what the reference's read_model raises on a non-.gmodel file (its
+        # unassigned locals), which get_TOAs takes as "spline model"
+        # (pptoas.py:375-378)
+        raise UnboundLocalError("%s is not a .gmodel file" % modelfile)
     ngauss = len(comps)
     params = np.zeros(ngauss * 6 + 2)
     flags = np.zeros(len(params))
@@ -231,6 +239,77 @@ def read_model_device(modelfile, nbin, freqs, P=None, quiet=False):
             return 0
         params[1] *= nbin / P
     return name, ngauss, gen_gaussian_portraits_device(code, params, alpha, nbin, freqs, nu_ref)
+
+
+# ---------------------------------------------------------------------------
+# B-spline (PCA) templates: ppspline.py models (host reader, device builder)
+# ---------------------------------------------------------------------------
+class _SplineUnpickler(pickle.Unpickler):
+    """Unpickler for ppspline model files (ppspline.py:206-228: a list of
+    name, source, datafile, mean_prof, eigvec and tck) that resolves only
+    numpy's array reconstruction: any other global in the file raises
+    UnpicklingError, so loading a model executes nothing it names."""
+
+    _ALLOWED = {("numpy.core.multiarray", "_reconstruct"),
+                ("numpy._core.multiarray", "_reconstruct"),
+                ("numpy.core.multiarray", "scalar"), ("numpy._core.multiarray", "scalar"),
+                ("numpy", "ndarray"), ("numpy", "dtype"),
+                ("_codecs", "encode")}  # protocol-2 bytes from Python 3
+
+    def find_class(self, module, name):
+        if (module, name) not in self._ALLOWED:
+            raise pickle.UnpicklingError("spline model: global %s.%s is not allowed"
+                                         % (module, name))
+        if name in ("ndarray", "dtype"):
+            return getattr(np, name)
+        if module == "_codecs":
+            import codecs
+            return codecs.encode
+        try:
+            from numpy._core import multiarray
+        except ImportError:  # numpy 1.x
+            from numpy.core import multiarray
+        return getattr(multiarray, name)
+
+
+def load_spline_model_file(modelfile):
+    """(modelname, source, datafile, mean_prof, eigvec, tck) of a ppspline
+    model: its Python-2 (or 3) pickle through _SplineUnpickler (latin-1 for
+    Python-2 strings), or an .npz holding the same fields."""
+    if str(modelfile).endswith(".npz"):
+        z = np.load(modelfile, allow_pickle=False)
+        tck = [z["t"], list(z["c"]), int(z["k"])]
+        return (str(z["modelname"]), str(z["source"]), str(z["datafile"]), z["mean_prof"],
+                z["eigvec"], tck)
+    with open(modelfile, "rb") as fh:
+        import warnings
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore", DeprecationWarning)
+            obj = _SplineUnpickler(fh, encoding="latin1").load()
+    modelname, source, datafile, mean_prof, eigvec, tck = obj
+    return modelname, source, datafile, np.asarray(mean_prof), np.asarray(eigvec), tck
+
+
+def gen_spline_portrait(mean_prof, freqs, eigvec, tck, nbin=None):
+    """gen_spline_portrait (pplib.py:932-956) on the device: FITPACK splev of
+    the projections at freqs, eigvec . proj + mean_prof, and the resample +
+    rotate when nbin != len(mean_prof) (ppf_spline_portraits).  Returns a
+    numpy array [nchan, nbin]."""
+    from .engine import get_engine
+    eigvec = np.asarray(eigvec)
+    return get_engine().spline_portraits(mean_prof, eigvec, tck, np.atleast_1d(freqs),
+                                         nbin).cpu().numpy()
+
+
+def read_spline_model(modelfile, freqs=None, nbin=None, quiet=False):
+    """read_spline_model (pplib.py:2961-2993): the model tuple, or (name,
+    portrait at freqs) built on the device."""
+    if not quiet:
+        print("Reading model from %s..." % modelfile)
+    modelname, source, datafile, mean_prof, eigvec, tck = load_spline_model_file(modelfile)
+    if freqs is None:
+        return modelname, source, datafile, mean_prof, eigvec, tck
+    return modelname, gen_spline_portrait(mean_prof, freqs, eigvec, tck, nbin)
 
 
 def write_model(filename, name, model_code, nu_ref, model_params, fit_flags, alpha,

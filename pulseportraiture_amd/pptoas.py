@@ -14,6 +14,7 @@ import numpy as np
 from . import archive as _arch
 from .mjd import MJD
 from .pplib import (DataBunch, F0_fact, phase_transform, guess_fit_freq, read_model,
+                    load_spline_model_file,
                     read_model_device, gen_gaussian_portraits_device, scattering_alpha,
                     weighted_mean, write_TOAs)
 from .pptoaslib import fit_portraits_batch, report_failure
@@ -99,7 +100,10 @@ class GetTOAs:
             if md.nbin != data.nbin or md.nchan != data.nchan:
                 return None
             return np.asarray(model)[None], np.zeros(nsub, dtype=np.int32), None
-        info = read_model(self.modelfile, quiet=True)
+        try:
+            info = read_model(self.modelfile, quiet=True)
+        except UnboundLocalError:  # not a .gmodel: a ppspline model (pptoas.py:375-378)
+            return self._spline_models(data)
         name, code, nu_ref, ngauss, gparams, mflags, alpha, fit_alpha = info
         self.model_name, self.ngauss = name, ngauss
         if fit_scat:
@@ -139,6 +143,52 @@ class GetTOAs:
                                                             nu_ref)
         return models, idx, None
 
+    def _spline_models(self, data):
+        """ppspline templates: read_spline_model(modelfile, freqs[isub], nbin)
+        per subint (pptoas.py:375-378), one device build per distinct channel
+        frequency row (ppf_spline_portraits)."""
+        name, source, datafile, mean_prof, eigvec, tck = load_spline_model_file(self.modelfile)
+        self.model_name = name
+        cache, keyf, idx = {}, [], np.zeros(data.nsub, dtype=np.int32)
+        for isub in data.ok_isubs:
+            f = data.freqs[isub]
+            idx[isub] = cache.setdefault(f.tobytes(), len(keyf))
+            if idx[isub] == len(keyf):
+                keyf.append(f)
+        from .engine import get_engine
+        models = get_engine().spline_portraits(mean_prof, eigvec, tck, np.array(keyf),
+                                               len(data.phases)).cpu().numpy()
+        return models, idx, None
+
+    def _irf_active(self):
+        return bool(getattr(self, "add_instrumental_response", False)) and \
+            bool(self.ird["DM"] or len(self.ird["wids"]))
+
+    def _irf_models(self, models, midx, data, isubs):
+        """Templates convolved with the instrumental response of each subint
+        (pptoas.py:387-393: instrumental_response_port_FT(nbin, freqsx, DM, P,
+        wids, irf_types) times rfft(modelx)), on the device.  The response
+        depends on the subint only through P (DM smearing) and chan_bw =
+        |freqsx[1] - freqsx[0]| of its ok channels; rows are convolved at
+        every channel (masked ones are not fitted).  A one-channel subint,
+        where the reference's chan_bw raises IndexError, gets chan_bw 0."""
+        from .engine import get_engine
+        eng = get_engine()
+        ird = self.ird
+        out, keys, idx = [], {}, np.zeros(data.nsub, dtype=np.int32)
+        for isub in isubs:
+            fx = data.freqs[isub, data.ok_ichans[isub]]
+            cbw = abs(fx[1] - fx[0]) if len(fx) > 1 else 0.0
+            P = data.Ps[isub]
+            key = (int(midx[isub]), data.freqs[isub].tobytes(), cbw, P if ird["DM"] else None)
+            if key not in keys:
+                keys[key] = len(out)
+                out.append(eng.instrumental_response_rows(
+                    models[midx[isub]], data.freqs[isub], ird["DM"], P, ird["wids"],
+                    ird["irf_types"], chan_bw=cbw).cpu().numpy())
+            idx[isub] = keys[key]
+        return np.stack(out), idx
+
     def get_TOAs(self, datafile=None, tscrunch=False, nu_refs=None, DM0=None, bary=True,
                  fit_DM=True, fit_GM=False, fit_scat=False, log10_tau=True, scat_guess=None,
                  fix_alpha=False, print_phase=False, print_flux=False, print_parangle=False,
@@ -147,8 +197,6 @@ class GetTOAs:
         """pptoas.py:150-738 with the subint loop batched on the device."""
         if quiet is None:
             quiet = self.quiet
-        if add_instrumental_response and (self.ird["DM"] or len(self.ird["wids"])):
-            raise NotImplementedError("instrumental response convolution (pptoas.py:387-393)")
         if tscrunch:
             raise NotImplementedError("tscrunch needs PSRCHIVE (out of scope)")
         already_warned = False
@@ -249,8 +297,6 @@ class GetTOAs:
         """
         if quiet is None:
             quiet = self.quiet
-        if add_instrumental_response and (self.ird["DM"] or len(self.ird["wids"])):
-            raise NotImplementedError("instrumental response convolution (pptoas.py:387-393)")
         if tscrunch:
             raise NotImplementedError("tscrunch needs PSRCHIVE (out of scope)")
         self.nfit = 1 + 2 * int(bool(fit_scat))
@@ -307,17 +353,33 @@ class GetTOAs:
             models, midx = [], {}
             rows, mrows, noise, where = [], [], [], []
             subints = np.asarray(data.subints)
+            irf = self._irf_active()
+            spline = None
             for isub in data.ok_isubs:
-                if self.is_FITS_model:
-                    key = 0
-                    if not models:
-                        models.append(model)
-                else:
-                    f = data.freqs[isub]
-                    key = midx.setdefault((f.tobytes(), data.Ps[isub]), len(models))
-                    if key == len(models):
-                        models.append(read_model_device(self.modelfile, nbin, f, data.Ps[isub],
-                                                        quiet=True)[2])
+                f = data.freqs[isub]
+                kk = ("fits",) if self.is_FITS_model else (f.tobytes(), data.Ps[isub])
+                if irf:  # modelx convolved per subint (pptoas.py:920-926)
+                    kk = kk + (int(isub),)
+                key = midx.setdefault(kk, len(models))
+                if key == len(models):
+                    if self.is_FITS_model:
+                        m = model
+                    else:
+                        try:
+                            m = read_model_device(self.modelfile, nbin, f, data.Ps[isub],
+                                                  quiet=True)[2]
+                        except UnboundLocalError:  # ppspline model (pptoas.py:912-915)
+                            if spline is None:
+                                spline = load_spline_model_file(self.modelfile)
+                            m = get_engine().spline_portraits(spline[3], spline[4], spline[5],
+                                                              f, nbin).cpu().numpy()
+                    if irf:
+                        fx = f[data.ok_ichans[isub]]
+                        cbw = abs(fx[1] - fx[0]) if len(fx) > 1 else 0.0
+                        m = get_engine().instrumental_response_rows(
+                            np.asarray(m, dtype=np.float64), f, self.ird["DM"], data.Ps[isub],
+                            self.ird["wids"], self.ird["irf_types"], chan_bw=cbw).cpu().numpy()
+                    models.append(m)
                 for ichan in data.ok_ichans[isub]:
                     if mweights is not None and mweights[ichan] == 0:
                         continue
@@ -345,13 +407,13 @@ class GetTOAs:
             covariances = z(nsub, nchan, self.nfit, self.nfit)
             nfevals = np.zeros([nsub, nchan], dtype="int")
             rcs = np.zeros([nsub, nchan], dtype="int")
-            for (isub, ichan), (phase, phase_err, scale, scale_err, snr, red_chi2) in zip(where, out):
+            for j, ((isub, ichan), (phase, phase_err, scale, scale_err, snr, red_chi2)) in \
+                    enumerate(zip(where, out)):
                 P = data.Ps[isub]
                 toa = data.epochs[isub] + MJD(((phase * P) + data.backend_delay) / (3600 * 24.))
                 toa_err = phase_err * P * 1e6
                 if print_flux:
-                    m = models[0 if self.is_FITS_model else
-                               mrows[where.index((isub, ichan))] // nchan][ichan]
+                    m = models[mrows[j] // nchan][ichan]
                     pfl[isub, ichan] = m.mean() * scale
                     pfle[isub, ichan] = abs(m.mean()) * scale_err
                 phis[isub, ichan], phi_errs[isub, ichan] = phase, phase_err
@@ -415,10 +477,9 @@ class GetTOAs:
                                rm_baseline=True, quiet=quiet)
         if data.dmc:
             raise RuntimeError("dedispersed archive: dededispersion needs PSRCHIVE")
-        if getattr(self, "add_instrumental_response", False) and \
-                (self.ird["DM"] or len(self.ird["wids"])):
-            raise NotImplementedError("instrumental response convolution (pptoas.py:1382-1388)")
         nbin = data.nbin
+        irf = self._irf_active()
+        spline = None
         subints = np.asarray(data.subints)
         models, mkeys = [], {}
         rows, ph, mrow, sc, taus, noise, where = [], [], [], [], [], [], []
@@ -439,6 +500,8 @@ class GetTOAs:
                 key = ("unscattered", freqs.tobytes())
             else:
                 key = ("model", freqs.tobytes())
+            if irf:  # the response depends on the subint (pptoas.py:1382-1388)
+                key = key + (int(isub),)
             if key not in mkeys:
                 mkeys[key] = len(models)
                 if self.is_FITS_model:
@@ -452,8 +515,22 @@ class GetTOAs:
                     gparams[1] = 0.0
                     m = gen_gaussian_portraits_device(info[1], gparams, 0.0, nbin, freqs, info[2])
                 else:
-                    m = read_model_device(self.modelfile, nbin, freqs, data.Ps.mean(),
-                                          quiet=True)[2]
+                    try:
+                        m = read_model_device(self.modelfile, nbin, freqs, data.Ps.mean(),
+                                              quiet=True)[2]
+                    except UnboundLocalError:  # ppspline model (pptoas.py:1380-1381)
+                        if spline is None:
+                            spline = load_spline_model_file(self.modelfile)
+                        from .engine import get_engine
+                        m = get_engine().spline_portraits(spline[3], spline[4], spline[5],
+                                                          freqs, nbin).cpu().numpy()
+                if irf:
+                    fx = freqs[data.ok_ichans[isub]]
+                    cbw = abs(fx[1] - fx[0]) if len(fx) > 1 else 0.0
+                    from .engine import get_engine
+                    m = get_engine().instrumental_response_rows(
+                        np.asarray(m, dtype=np.float64), freqs, self.ird["DM"], P,
+                        self.ird["wids"], self.ird["irf_types"], chan_bw=cbw).cpu().numpy()
                 models.append(np.asarray(m, dtype=np.float64))
             k = mkeys[key]
             phs = phase_shifts(phi, DM, GM, freqs, nu_ref_DM, nu_ref_GM, P)
@@ -585,6 +662,8 @@ class GetTOAs:
                 print("Model nbin/nchan mismatch for %s; skipping it." % datafile)
             return None
         models, midx, _ = mm
+        if self._irf_active():
+            models, midx = self._irf_models(models, midx, data, ok_isubs)
         mask = np.zeros((nsub, nchan), dtype=np.uint8)
         for isub in ok_isubs:
             mask[isub, data.ok_ichans[isub]] = 1

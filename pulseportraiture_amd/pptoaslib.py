@@ -14,7 +14,8 @@ import numpy as np
 from .pplib import (DataBunch, Dconst, RCSTRINGS, scattering_times,
                     scattering_portrait_FT)
 
-__all__ = ["fit_portrait_full", "fit_portraits_batch", "phase_shifts",
+__all__ = ["fit_portrait_full", "fit_portraits_batch", "instrumental_response_FT",
+           "instrumental_response_port_FT", "phase_shifts",
            "phase_shifts_deriv", "rotate_portrait_full", "scattering_times",
            "scattering_portrait_FT"]
 
@@ -49,6 +50,26 @@ def rotate_portrait_full(port, phi, DM, GM, freqs, nu_DM=np.inf, nu_GM=np.inf, P
         P = 1.0
     ph = phase_shifts(phi, DM, GM, np.asarray(freqs, dtype=float), nu_DM, nu_GM, P)
     return get_engine().rotate_rows(np.asarray(port, dtype=float), ph).cpu().numpy()
+
+
+def instrumental_response_port_FT(nbin, freqs, DM=0.0, P=1.0, wids=[], irf_types=[]):
+    """pptoaslib.py:145-179 on the device: the [nchan, nharm] product of the
+    responses ('rect' np.sinc(k wid), 'gauss' the normalised Gaussian FT of
+    FWHM wid) and, for DM != 0, the rect smearing of width 8.3e-6 chan_bw /
+    (freq / 1e3)^3 / P (the reference's formula, where DM only switches it
+    on).  Returned real (the reference's imaginary parts are zero)."""
+    from .engine import get_engine
+    freqs = np.atleast_1d(np.asarray(freqs, dtype=np.float64))
+    if DM == len(wids) == 0.0:
+        return np.ones([len(freqs), nbin // 2 + 1])
+    return get_engine().response_table(nbin, freqs, DM, P, wids, irf_types).cpu().numpy()
+
+
+def instrumental_response_FT(nbin, wid=0.0, irf_type="rect"):
+    """pptoaslib.py:112-143: one response row (wid 0 -> ones)."""
+    if wid == 0.0:
+        return np.ones(nbin // 2 + 1)
+    return instrumental_response_port_FT(nbin, [1.0], 0.0, 1.0, [wid], [irf_type])[0]
 
 
 def _nan(v):

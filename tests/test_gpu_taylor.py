@@ -182,3 +182,29 @@ def test_taylor_vs_oracle_headline_masked(eng):
         assert out["param_errs"][i][0] == pytest.approx(ref.phi_err, rel=1e-6)
         assert out["red_chi2"][i] == pytest.approx(ref.red_chi2, rel=1e-9)
         assert np.all(out["scales"][i][~ok] == 0.0)
+
+
+@pytest.mark.parametrize("pieces", [2, 3, 8])
+def test_pipeline_pieces_bitwise(eng, pieces):
+    """The two-queue piece pipeline (ppf_set_pipeline) runs the same kernels on
+    disjoint workspace slices: results are bitwise those of one queue, also
+    for a chunk smaller than the batch (workspace limit) and ragged pieces."""
+    nsub = 301
+    w = synth.make_workload(nsub, 64, 2048, seed=123)
+    data = synth.workload_data_host(w)
+    nu = O.guess_fit_freq(w.freqs)
+    args = (data, w.model, w.freqs, w.P, [0.0, w.DM0, 0, 0, 0], [1, 1, 0, 0, 0])
+    try:
+        eng.set_pipeline(1)
+        ref = _np(eng.fit_batch(*args, nu_fit=[nu, nu, nu], guess=True))
+        eng.set_pipeline(pieces)
+        out = _np(eng.fit_batch(*args, nu_fit=[nu, nu, nu], guess=True))
+        eng.set_workspace_limit(120 * 1100 * 1024)  # chunks of ~110 subints
+        out2 = _np(eng.fit_batch(*args, nu_fit=[nu, nu, nu], guess=True))
+    finally:
+        eng.set_pipeline(0)
+        eng.set_workspace_limit(32 << 30)
+    for o in (out, out2):
+        for k in ["params", "param_errs", "nu_out", "cov", "scales", "red_chi2", "snr", "nfev",
+                  "status"]:
+            np.testing.assert_array_equal(o[k], ref[k], err_msg=k)

@@ -1,0 +1,106 @@
+"""Device template producers against the reference (tests/golden/
+make_golden_r3.py): ppf_spline_portraits (gen_spline_portrait,
+pplib.py:932-956, incl. the resample + rotate branch), ppf_instrumental_
+response_rows (instrumental_response_port_FT, pptoaslib.py:145-179) and
+get_TOAs with a ppspline model and with add_instrumental_response.
+
+Tolerances: templates within 1e-12 of their peak (device exp/sin/erf and the
+dgemm-vs-fused eigenvector sum differ from glibc/BLAS in the last bits);
+fitted parameters within the north_star 1e-3 sigma, identical return codes,
+.tim lines as in test_gpu_configs."""
+import json
+import os
+import shutil
+
+import numpy as np
+import pytest
+
+from tests.conftest import GOLDEN
+from tests.test_gpu_configs import compare_tim, register_synth_archive
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from pulseportraiture_amd.engine import get_engine
+    return get_engine(0)
+
+
+@pytest.fixture(scope="module")
+def fx():
+    return (np.load(os.path.join(GOLDEN, "templates_r3.npz")),
+            json.load(open(os.path.join(GOLDEN, "templates_r3.json"))))
+
+
+@pytest.mark.parametrize("name", ["m3", "m5", "m1", "m0"])
+def test_spline_portraits(gpu, fx, name, tmp_path):
+    from pulseportraiture_amd import pplib
+    z, meta = fx
+    path = tmp_path / (name + ".spl")
+    path.write_bytes(bytes(z["spl_%s_file" % name]))
+    for tag in meta[name]["cases"]:
+        p = "spl_%s_%s_" % (name, tag)
+        mn, port = pplib.read_spline_model(str(path), z[p + "freqs"], int(z[p + "nbin"]),
+                                           quiet=True)
+        ref = z[p + "port"]
+        assert port.shape == ref.shape
+        err = np.max(np.abs(port - ref)) / np.max(np.abs(ref))
+        assert err <= 1e-12, (name, tag, err)
+
+
+def test_instrumental_response_tables(gpu, fx):
+    from pulseportraiture_amd import pptoaslib
+    z, meta = fx
+    for tag in ["rect", "gauss", "both_dm", "dm"]:
+        m = meta["irf_" + tag]
+        R = pptoaslib.instrumental_response_port_FT(m["nbin"], z["irf_%s_freqs" % tag], m["DM"],
+                                                    m["P"], m["wids"], m["irf_types"])
+        np.testing.assert_allclose(R, np.real(z["irf_" + tag]), rtol=0, atol=1e-14)
+
+
+def test_instrumental_response_rows_linear(gpu):
+    """Convolution is linear and the identity response returns the rows."""
+    rng = np.random.default_rng(5)
+    rows = rng.normal(size=(6, 512))
+    f = np.linspace(1200.0, 1800.0, 6)
+    a = gpu.instrumental_response_rows(rows, f, 1.0, 0.002, [0.01], ["gauss"]).cpu().numpy()
+    b = gpu.instrumental_response_rows(2.0 * rows, f, 1.0, 0.002, [0.01], ["gauss"]).cpu().numpy()
+    np.testing.assert_allclose(b, 2.0 * a, rtol=0, atol=1e-12)
+    R = gpu.response_table(512, f, 1.0, 0.002, [0.01], ["gauss"]).cpu().numpy()
+    ref = np.fft.irfft(R * np.fft.rfft(rows, axis=-1), axis=-1)
+    np.testing.assert_allclose(a, ref, rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize("tag", ["spline", "spline_up", "irf", "irf_dmonly"])
+def test_get_toas_templates(gpu, fx, tag, tmp_path):
+    from pulseportraiture_amd import pplib, pptoas, synth
+    z, meta = fx
+    a = meta["gt_archive"]
+    register_synth_archive(a["name"], a["nsub"], a["nchan"], a["nbin"], a["seed"], 0.0, 0.0)
+    m = meta["gt_" + tag]
+    shutil.copy(synth.EXAMPLE_GMODEL, os.path.join(tmp_path, "example.gmodel"))
+    for name in ["m3", "m5", "m1", "m0"]:
+        (tmp_path / (name + ".spl")).write_bytes(bytes(z["spl_%s_file" % name]))
+    cwd = os.getcwd()
+    os.chdir(tmp_path)
+    try:
+        gt = pptoas.GetTOAs([a["name"]], m["model"], quiet=True)
+        if m["ird"] is not None:
+            gt.ird = gt.instrumental_response_dict = dict(m["ird"])
+        gt.get_TOAs(quiet=True, **m["kwargs"])
+        lines = [pplib.toa_line(t) for t in gt.TOA_list]
+    finally:
+        os.chdir(cwd)
+    p = "gt_%s_" % tag
+    assert np.array_equal(gt.rcs[0], z[p + "rcs"])
+    for par, err in [("phis", "phi_errs"), ("DMs", "DM_errs"), ("GMs", "GM_errs")]:
+        e = z[p + err]
+        if np.all(e > 0):
+            assert np.all(np.abs(gt.__dict__[par][0] - z[p + par]) <= 1e-3 * e), par
+    np.testing.assert_allclose(gt.snrs[0], z[p + "snrs"], rtol=1e-6)
+    np.testing.assert_allclose(gt.red_chi2s[0], z[p + "red_chi2s"], rtol=1e-8)
+    compare_tim(lines, m["tim"])
