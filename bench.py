@@ -233,8 +233,12 @@ def main():
         else:
             bytes_launch = nsub * nharm * 16.0 * 2
             what = "k_guess: R and mean-template spectra"
+        lps = max(n / args.steps, 1.0) if dom != "solve" else 1.0
+        bytes_launch /= lps  # the chunk may run as several pieces (ppf_set_pipeline)
         achieved = bytes_launch / avg_s / 1e9
         traffic = pmc_traffic(dom, nsub, nbin, nchan, args.config)
+        if traffic:
+            traffic /= lps
         roof = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic, "traffic_unit": "bytes/launch",
@@ -250,9 +254,9 @@ def main():
     others = {}
     taylor = not flags[3] and tau == 0.0
     if ktimes:
-        def avg_ms(k):
+        def avg_ms(k):  # per step's worth of subints (all pieces of the chunk)
             ms, n = ktimes[k]
-            return ms / max(n, 1)
+            return ms / max(n, 1) * max(n / args.steps, 1.0)
         if taylor and ktimes.get("moments", (0, 0))[1]:
             t = avg_ms("moments") / 1e3
             # T = V (32 x nharm powers v^m) . W (nharm x 2 nchan), fp64 MFMA

@@ -259,6 +259,13 @@ int ppf_instrumental_response_rows(ppf_ctx* ctx, int32_t nrow, int32_t nbin, con
                                    double DM, double chan_bw, double P, const double* freqs,
                                    double* out);
 
+/* tscrunch (load_data's arch.tscrunch(), pplib.py:2700) of fold-mode
+ * subints: out[p][n][j] = sum_s w[s][n] data[s][p][n][j] / sum_s w[s][n]
+ * (0 where the weights sum to 0), wsum[n] = sum_s w[s][n] (NULL: not
+ * written).  data [nsub][npol][nchan][nbin], weights [nsub][nchan].      */
+int ppf_tscrunch(ppf_ctx* ctx, int32_t nsub, int32_t npol, int32_t nchan, int32_t nbin,
+                 const double* data, const double* weights, double* out, double* wsum);
+
 /* PSRFITS samples to physical values (PSRCHIVE's load + pscrunch in
  * load_data, pplib.py:2670-2732): raw [nsub][npol][nchan][nbin] of
  * raw_type (ppfits.h PPFITS_RAW_*: 1 uint8, 2 int16, 3 float32), scl and

@@ -78,6 +78,47 @@ def normalize(b, name="archive"):
     return b
 
 
+def tscrunch(b, period_at=None):
+    """arch.tscrunch() as load_data applies it (pplib.py:2700) to a normalised
+    archive: one subint whose profiles are the weight-averaged profiles of
+    all subints (fold-mode subints share the predictor's phase, so they add
+    without rotation), weights summed per channel (ppf_tscrunch, on the
+    device).  Epoch: the duration-weighted mean epoch (the middle of the span
+    for contiguous equal subints); duration: the sum; period: period_at(epoch
+    in days) when the archive has a predictor (PSRFITS POLYCO), else the
+    duration-weighted mean; Doppler factor, parallactic angle and SNRs: the
+    (duration-weighted) means.  PSRCHIVE recomputes some of these from the
+    ephemeris and its own estimators, which this build does not have: parity
+    with PSRCHIVE is unpinned (DESIGN.md)."""
+    from .engine import get_engine
+    b = normalize(b, b.get("filename", "archive"))
+    if b.nsub == 1:
+        return b
+    sub, ws = get_engine().tscrunch(b.subints, b.weights)
+    dur = np.asarray(b.subtimes, dtype=np.float64)
+    wt = dur / dur.sum() if dur.sum() > 0 else np.full(b.nsub, 1.0 / b.nsub)
+    e0 = b.epochs[0]
+    offs = np.array([(e.days - e0.days) * 86400.0 + (e.secs - e0.secs) +
+                     (e.fracsec - e0.fracsec) for e in b.epochs])
+    epoch = e0 + float(np.sum(wt * offs))
+    out = DataBunch(**dict(b))
+    out.subints = sub.cpu().numpy()
+    out.weights = ws.cpu().numpy()
+    out.nsub = 1
+    out.epochs = [epoch]
+    out.subtimes = [float(dur.sum())]
+    out.Ps = np.array([period_at(epoch.in_days()) if period_at is not None
+                       else float(np.sum(wt * b.Ps))])
+    out.freqs = b.freqs[:1]
+    out.doppler_factors = np.array([float(np.sum(wt * np.asarray(b.doppler_factors)))])
+    out.parallactic_angles = np.array([float(np.sum(wt * np.asarray(b.parallactic_angles)))])
+    out.SNRs = np.sqrt(np.sum(np.asarray(b.SNRs) ** 2, axis=0))[None]
+    out.noise_stds = None  # re-estimated from the averaged profiles (use_get_noise)
+    for k in ["ok_isubs", "ok_ichans", "masks"]:
+        out.pop(k, None)
+    return normalize(out, b.filename)
+
+
 ARRAY_KEYS = ["subints", "freqs", "weights", "Ps", "SNRs", "doppler_factors",
               "parallactic_angles", "noise_stds", "subtimes"]
 SCALAR_KEYS = ["DM", "dmc", "backend", "frontend", "backend_delay", "telescope",
@@ -110,7 +151,8 @@ def load_data(filename, **kw):
     if isinstance(filename, dict):
         return normalize(filename)
     if filename in _registry:
-        return _registry[filename]
+        b = _registry[filename]
+        return tscrunch(b) if kw.get("tscrunch") else b
     if isinstance(filename, str) and is_fits(filename):
         from .psrfits import load_psrfits
         return normalize(load_psrfits(filename, pscrunch=kw.get("pscrunch", False),
@@ -128,7 +170,8 @@ def load_data(filename, **kw):
         for k in ["dmc"]:
             if k in b:
                 b[k] = int(b[k])
-        return normalize(b, filename)
+        b = normalize(b, filename)
+        return tscrunch(b) if kw.get("tscrunch") else b
     raise RuntimeError("Cannot load_data(%s): not a registered, .npz or PSRFITS archive "
                        "(other PSRCHIVE formats need PSRCHIVE)" % filename)
 

@@ -907,6 +907,19 @@ int ppf_instrumental_response_rows(ppf_ctx* ctx, int32_t nrow, int32_t nbin, con
   });
 }
 
+int ppf_tscrunch(ppf_ctx* ctx, int32_t nsub, int32_t npol, int32_t nchan, int32_t nbin,
+                 const double* data, const double* weights, double* out, double* wsum) {
+  if (!ctx || !data || !weights || !out) return fail(ctx, PPF_ERR_INVALID, "null argument");
+  if (nsub <= 0 || npol <= 0 || nchan <= 0 || nbin <= 0)
+    return fail(ctx, PPF_ERR_INVALID, "empty archive (%d, %d, %d, %d)", nsub, npol, nchan, nbin);
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  const size_t total = (size_t)npol * nchan * nbin;
+  return timed(ctx, PPF_K_MODEL_FFT, [&] {
+    hipLaunchKernelGGL(k_tscrunch, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, ctx->stream,
+                       data, weights, nsub, npol, nchan, nbin, out, wsum);
+  });
+}
+
 int ppf_irfft_rows(ppf_ctx* ctx, int32_t nrow, int32_t nbin, const double* spec, double* out) {
   if (!ctx || !spec || !out) return fail(ctx, PPF_ERR_INVALID, "null argument");
   if (nrow <= 0) return PPF_OK;

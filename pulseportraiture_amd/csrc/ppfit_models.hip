@@ -264,6 +264,32 @@ __global__ void k_ir_spec(double2* __restrict__ spec, double* __restrict__ resp,
 }
 
 // ---------------------------------------------------------------------------
+// tscrunch of fold-mode subints (load_data's arch.tscrunch(), pplib.py:2700):
+// per (pol, channel, bin) the weight-averaged profile over the subints,
+// out = sum_s w[s][n] d[s][p][n][j] / sum_s w[s][n] (0 where the weights sum
+// to 0), and wsum[n] = sum_s w[s][n].  One thread per output sample, the
+// subint loop in order (coalesced along the bins).
+// ---------------------------------------------------------------------------
+__global__ void k_tscrunch(const double* __restrict__ d, const double* __restrict__ w, int nsub,
+                           int npol, int nchan, int nbin, double* __restrict__ out,
+                           double* __restrict__ wsum) {
+  const size_t total = (size_t)npol * nchan * nbin;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int j = (int)(i % nbin);
+  const int n = (int)((i / nbin) % nchan);
+  const int p = (int)(i / ((size_t)nbin * nchan));
+  double acc = 0.0, ws = 0.0;
+  for (int s = 0; s < nsub; ++s) {
+    const double ww = w[(size_t)s * nchan + n];
+    if (ww != 0.0) acc = fma(ww, d[(((size_t)s * npol + p) * nchan + n) * nbin + j], acc);
+    ws += ww;
+  }
+  out[i] = ws != 0.0 ? acc / ws : 0.0;
+  if (p == 0 && j == 0 && wsum) wsum[n] = ws;
+}
+
+// ---------------------------------------------------------------------------
 // PSRFITS unpacking (load_data's Archive_load + pscrunch, pplib.py:2670-2732):
 // out[s][q][n][j] = sum over the polarisations q takes of
 //   raw[s][p][n][j] * scl[s][p][n] + offs[s][p][n]

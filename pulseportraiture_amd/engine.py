@@ -441,6 +441,21 @@ class Engine:
         out._keep = f
         return out
 
+    def tscrunch(self, subints, weights):
+        """Weight-averaged subint (ppf_tscrunch): subints [nsub, npol, nchan,
+        nbin], weights [nsub, nchan] -> ([1, npol, nchan, nbin], [1, nchan])
+        device tensors."""
+        dev = self.device
+        d = _dev_f64(subints, dev).contiguous()
+        w = _dev_f64(weights, dev).contiguous()
+        nsub, npol, nchan, nbin = d.shape
+        out = torch.empty((1, npol, nchan, nbin), dtype=torch.float64, device=dev)
+        ws = torch.empty((1, nchan), dtype=torch.float64, device=dev)
+        self._chk(self.lib.ppf_tscrunch(self.ctx, nsub, npol, nchan, nbin, _ptr(d), _ptr(w),
+                                        _ptr(out), _ptr(ws)))
+        out._keep = (d, w)
+        return out, ws
+
     def irfft_rows(self, spec, nbin):
         dev = self.device
         if isinstance(spec, torch.Tensor) and spec.is_complex():

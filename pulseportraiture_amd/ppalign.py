@@ -48,12 +48,12 @@ def allreduce_sum(*tensors):
     return tensors
 
 
-def _units(datafiles, model_data, SNR_cutoff, quiet, skip_these, state=None):
+def _units(datafiles, model_data, SNR_cutoff, quiet, skip_these, state=None, tscrunch=False):
     """Load archives and list (archive, subint, ichans, model_ichans) units."""
     units, archives = [], {}
     for name in datafiles:
         try:
-            data = _arch.load_data(name)
+            data = _arch.load_data(name, tscrunch=tscrunch)  # ppalign.py:123-127
         except RuntimeError:
             if not quiet:
                 print("%s: cannot load_data().  Skipping it." % name)
@@ -96,15 +96,13 @@ def align_archives(metafile, initial_guess, fit_dm=True, tscrunch=False, pscrunc
     .npz).
     """
     from .engine import get_engine
-    if tscrunch:
-        raise NotImplementedError("tscrunch needs PSRCHIVE (out of scope)")
     if isinstance(metafile, str) and _arch.file_is_type(metafile, "ASCII"):
         datafiles = [ln.strip() for ln in open(metafile).readlines() if ln.strip()]
         if outfile is None:
             outfile = metafile + ".algnd.fits"
     else:
         datafiles = list(metafile) if not isinstance(metafile, str) else [metafile]
-    model_data = _arch.load_data(initial_guess)
+    model_data = _arch.load_data(initial_guess, tscrunch=True)  # ppalign.py:103-106
     npol = 1 if pscrunch else model_data.npol
     model_port = np.asarray((model_data.masks * model_data.subints)[0, 0], dtype=np.float64)
     nchan, nbin = model_port.shape
@@ -113,7 +111,8 @@ def align_archives(metafile, initial_guess, fit_dm=True, tscrunch=False, pscrunc
     dev = eng.device
     rank, world = dist_info()
     skip_these = []
-    units, archives = _units(datafiles, model_data, SNR_cutoff, quiet, skip_these)
+    units, archives = _units(datafiles, model_data, SNR_cutoff, quiet, skip_these,
+                             tscrunch=tscrunch)
     lo, hi = shard_range(len(units), rank, world)
     mine = units[lo:hi]
     count = 1

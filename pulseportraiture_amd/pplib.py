@@ -254,7 +254,8 @@ class _SplineUnpickler(pickle.Unpickler):
                 ("numpy._core.multiarray", "_reconstruct"),
                 ("numpy.core.multiarray", "scalar"), ("numpy._core.multiarray", "scalar"),
                 ("numpy", "ndarray"), ("numpy", "dtype"),
-                ("_codecs", "encode")}  # protocol-2 bytes from Python 3
+                ("_codecs", "encode"),  # protocol-2 bytes from Python 3
+                ("__builtin__", "bytes"), ("builtins", "bytes")}  # ... and empty ones
 
     def find_class(self, module, name):
         if (module, name) not in self._ALLOWED:
@@ -265,6 +266,8 @@ class _SplineUnpickler(pickle.Unpickler):
         if module == "_codecs":
             import codecs
             return codecs.encode
+        if name == "bytes":
+            return bytes
         try:
             from numpy._core import multiarray
         except ImportError:  # numpy 1.x

@@ -197,8 +197,6 @@ class GetTOAs:
         """pptoas.py:150-738 with the subint loop batched on the device."""
         if quiet is None:
             quiet = self.quiet
-        if tscrunch:
-            raise NotImplementedError("tscrunch needs PSRCHIVE (out of scope)")
         already_warned = False
         warning = "You are using an experimental functionality of pptoas!"
         self.nfit = 1 + int(fit_DM) + int(fit_GM) + 2 * int(fit_scat) - int(fix_alpha)
@@ -297,8 +295,6 @@ class GetTOAs:
         """
         if quiet is None:
             quiet = self.quiet
-        if tscrunch:
-            raise NotImplementedError("tscrunch needs PSRCHIVE (out of scope)")
         self.nfit = 1 + 2 * int(bool(fit_scat))
         self.fit_phi, self.fit_tau = True, fit_scat
         self.fit_flags = [int(self.fit_phi), int(self.fit_tau)]

@@ -181,9 +181,6 @@ def pscrunch_mode(npol, pol_type):
 def load_psrfits(path, pscrunch=True, dededisperse=False, tscrunch=False, rm_baseline=False,
                  quiet=True, engine=None):
     """pplib.load_data (pplib.py:2650-2820) for a fold-mode PSRFITS archive."""
-    if tscrunch:
-        raise NotImplementedError("tscrunch of a PSRFITS archive (PSRCHIVE's tscrunch needs the "
-                                  "predictor to realign subints): out of scope")
     if dededisperse:
         raise NotImplementedError("dededispersion needs PSRCHIVE")
     from .engine import get_engine
@@ -236,6 +233,9 @@ def load_psrfits(path, pscrunch=True, dededisperse=False, tscrunch=False, rm_bas
                  telescope_code=TELESCOPE_CODES.get(tel.upper(), tel),
                  bw=float(I.obsbw), nu0=float(I.obsfreq), subtimes=list(meta["tsubint"]),
                  source=f.text("source") or "noname", state=state, filename=path)
+    if tscrunch:  # arch.tscrunch() (pplib.py:2700); the POLYCO gives P at the new epoch
+        from .archive import tscrunch as _tscrunch
+        bunch = _tscrunch(bunch, None if pc is None else (lambda mjd: polyco_period(pc, mjd)))
     if not quiet:
         print("\nReading data from %s on source %s..." % (path, bunch["source"]))
     return bunch

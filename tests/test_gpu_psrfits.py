@@ -91,3 +91,44 @@ def test_get_toas_psrfits_equals_registered(gpu, tmp_path):
     finally:
         os.chdir(cwd)
     assert len(lines[0]) == 3 and lines[0] == lines[1]
+
+
+def test_tscrunch_psrfits_and_get_toas(gpu, tmp_path):
+    """load_data(tscrunch=True) (pplib.py:2700): one subint, the weight-averaged
+    profiles (channel 5 of subint 2 has weight 0), summed weights, the
+    duration-weighted mean epoch; get_TOAs(tscrunch=True) fits that subint,
+    equal to fitting the same averaged archive registered in memory.  The
+    semantics restate PSRCHIVE's weighted tscrunch; parity with PSRCHIVE itself
+    is unpinned (not in this image)."""
+    from pulseportraiture_amd import archive, pplib, pptoas, synth
+    path = str(tmp_path / "ts.fits")
+    w, raw, scl, offs, wts = _coherence_archive(path, nsub=4, nchan=32, nbin=512, seed=31)
+    full = archive.load_data(path, pscrunch=True)
+    d = archive.load_data(path, pscrunch=True, tscrunch=True)
+    sub = np.asarray(full.subints)[:, 0]
+    ww = np.asarray(full.weights)
+    want = np.einsum("sn,snj->nj", ww, sub) / ww.sum(0)[:, None]
+    assert d.nsub == 1 and np.asarray(d.subints).shape == (1, 1, 32, 512)
+    np.testing.assert_allclose(np.asarray(d.subints)[0, 0], want, rtol=0,
+                               atol=1e-13 * np.abs(want).max())
+    np.testing.assert_array_equal(d.weights[0], ww.sum(0))
+    mid = np.mean([e.in_days() for e in full.epochs])
+    assert abs(d.epochs[0].in_days() - mid) < 1e-11
+    assert d.subtimes[0] == 120.0 and abs(d.Ps[0] - w.P) < 1e-15
+    reg = {k: d[k] for k in ["subints", "freqs", "weights", "Ps", "epochs", "SNRs",
+                             "doppler_factors", "parallactic_angles", "DM", "dmc", "backend",
+                             "frontend", "backend_delay", "telescope", "telescope_code", "bw",
+                             "nu0", "subtimes", "source", "state"]}
+    archive.register_archive("ts_registered", reg)
+    shutil.copy(synth.EXAMPLE_GMODEL, str(tmp_path / "example.gmodel"))
+    cwd = os.getcwd()
+    os.chdir(tmp_path)
+    try:
+        lines = []
+        for name, ts in [(path, True), ("ts_registered", False)]:
+            gt = pptoas.GetTOAs([name], "example.gmodel", quiet=True)
+            gt.get_TOAs(quiet=True, tscrunch=ts)
+            lines.append([pplib.toa_line(t).split(None, 1)[1] for t in gt.TOA_list])
+    finally:
+        os.chdir(cwd)
+    assert len(lines[0]) == 1 and lines[0] == lines[1]

@@ -38,6 +38,11 @@ def test_oracle_spline_portraits(fx):
 def test_spline_file_reader(fx, tmp_path):
     from pulseportraiture_amd.pplib import load_spline_model_file, read_model
     z, _ = fx
+    for name in ["m3", "m5", "m1", "m0"]:  # every model the fixtures hold loads
+        path = tmp_path / (name + ".spl")
+        path.write_bytes(bytes(z["spl_%s_file" % name]))
+        mn, src, df, mean, eigvec, tck = load_spline_model_file(str(path))
+        assert mn == name + ".spl"
     path = tmp_path / "m3.spl"
     path.write_bytes(bytes(z["spl_m3_file"]))
     mn, src, df, mean, eigvec, tck = load_spline_model_file(str(path))
