@@ -7,7 +7,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 SOURCES = ["ppfit_lib.hip"]
-DEPS = ["ppfit_lib.hip", "ppfit_spectra.hip", "ppfit_fit.hip", "ppfit_taylor.hip", "ppfit_tnc.hip", "ppfit_models.hip", "ppfit_capi.hip",
+DEPS = ["ppfit_lib.hip", "ppfit_spectra.hip", "ppfit_fit.hip", "ppfit_taylor.hip", "ppfit_tnc.hip", "ppfit_ncg.hip", "ppfit_models.hip", "ppfit_capi.hip",
         "ppfit_kernels.hpp", "ppfit_device.hpp"]
 OUT = os.path.join(HERE, "libppfit.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

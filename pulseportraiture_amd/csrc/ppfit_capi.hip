@@ -347,7 +347,8 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
     return fail(ctx, PPF_ERR_UNSUPPORTED, "nchan=%d outside [1, %d]", d->nchan, PPF_MAX_NCHAN);
   if (d->nmodel <= 0) return fail(ctx, PPF_ERR_INVALID, "nmodel must be >= 1");
   const bool tnc = d->method == PPF_METHOD_TNC || d->method == PPF_METHOD_TNC_LEGACY;
-  if (d->method != PPF_METHOD_TRUST_NCG && !tnc)
+  const bool ncg = d->method == PPF_METHOD_NEWTON_CG;
+  if (d->method != PPF_METHOD_TRUST_NCG && !tnc && !ncg)
     return fail(ctx, PPF_ERR_UNSUPPORTED, "Method %d is not implemented.", d->method);
   if (d->method == PPF_METHOD_TNC_LEGACY &&
       !(d->fit_flags[0] && d->fit_flags[1] && !d->fit_flags[2] && !d->fit_flags[3] &&
@@ -616,13 +617,18 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
             hipLaunchKernelGGL(k_tnc<true>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
             return;
           }
+          if (ncg) {
+            hipLaunchKernelGGL(k_ncg<false>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
+            hipLaunchKernelGGL(k_ncg<true>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
+            return;
+          }
           if (exact)
             hipLaunchKernelGGL(k_solve<false>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
           if (!split_scat)
             hipLaunchKernelGGL(k_solve<true>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
         }))
       return r;
-    if (split_scat && !tnc) {
+    if (split_scat && !tnc && !ncg) {
       // k_solve<true> with each evaluation over `split` blocks per subint
       double* part = static_cast<double*>(ctx->spart.p);
       int* active = reinterpret_cast<int*>(part + (size_t)nc * ((nchan + 7) / 8) * kScatPart);

@@ -461,6 +461,7 @@ __global__ void k_moments(FitArgs a);
 __global__ void k_selftest(int* fails);
 template <bool SCAT> __global__ void k_solve(FitArgs a);
 template <bool SCAT> __global__ void k_tnc(FitArgs a);
+template <bool SCAT> __global__ void k_ncg(FitArgs a);
 template <bool SCAT> __global__ void k_post(FitArgs a);
 
 }  // namespace ppf

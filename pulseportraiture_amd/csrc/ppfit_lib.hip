@@ -3,5 +3,6 @@
 #include "ppfit_fit.hip"
 #include "ppfit_taylor.hip"
 #include "ppfit_tnc.hip"
+#include "ppfit_ncg.hip"
 #include "ppfit_models.hip"
 #include "ppfit_capi.hip"

@@ -303,3 +303,51 @@ def test_legacy_fit_portrait_tnc(eng, golden, ic):
     np.testing.assert_allclose(r.scale_errs, g[k + "scale_errs"], rtol=1e-8)
     print("legacy TNC %d: status %d (reference %d), nfev %d (reference %d)" % (
         ic, r.return_code, ref_rc, r.nfeval, int(g[k + "nfeval"])))
+
+
+# ---------------------------------------------------------------------------
+# Newton-CG (pptoaslib.py:1003-1004: jac, hess, maxiter 2000, xtol -1)
+# ---------------------------------------------------------------------------
+def test_fit_full_r2_newton_cg_golden(eng, golden):
+    """The device Newton-CG (ppfit_ncg.hip) against the reference's own
+    Newton-CG fit (fit_full_r2.npz case 10): status 2 (line search at the
+    rounding floor), parameters within 1e-3 sigma, errors and covariance."""
+    f = golden("fit_full_r2.npz")
+    r = fit_r2(eng, f, 10)
+    assert_fit_matches(r, f, 10)
+    print("Newton-CG: nfev %d (reference %d)" % (int(r["nfev"][0]), int(f["f10_nfeval"])))
+
+
+@pytest.mark.parametrize("ic", [0, 1, 2, 3, 4, 5])
+def test_newton_cg_vs_oracle(eng, golden, ic):
+    """Newton-CG on every trust-ncg fixture input (phase+GM, scattering with
+    log10 tau, GM + tau, masked channels...) against the oracle's scipy
+    Newton-CG on the same input: identical status, fitted parameters within
+    1e-3 sigma (phase compared at a common frequency)."""
+    from oracle import ppfit_oracle as O
+    from tests._compare import phase_gap
+    f = golden("fit_full_r2.npz")
+    k = "f%d_" % ic
+    flags = [int(v) for v in f[k + "flags"]]
+    nu = float(f[k + "nu_fit"])
+    r = _np(eng.fit_batch(f[k + "data"], f[k + "model"], f[k + "freqs"], float(f["P"]),
+                          f[k + "init"], flags, nu_fit=[nu, nu, nu], errs=f[k + "errs"],
+                          log10_tau=bool(f[k + "log10"]), option=int(f[k + "option"]),
+                          method="Newton-CG"))
+    ref = O.fit_portrait_full(f[k + "data"], f[k + "model"], list(f[k + "init"]), float(f["P"]),
+                              f[k + "freqs"], [nu] * 3, [None] * 3, f[k + "errs"], flags,
+                              log10_tau=bool(f[k + "log10"]), option=int(f[k + "option"]),
+                              method="Newton-CG")
+    assert int(r["status"][0]) == ref.return_code, (int(r["status"][0]), ref.return_code)
+    p = r["params"][0]
+    if flags[0]:
+        refd = {"phi": ref.phi, "phi_err": ref.phi_err, "nu_DM": ref.nu_DM, "nu_GM": ref.nu_GM}
+        assert phase_gap(p[0], p[1], p[2], r["nu_out"][0][0], r["nu_out"][0][1], refd,
+                         float(f["P"])) <= 1e-3
+    for i, nm in enumerate(["DM", "GM", "tau", "alpha"], start=1):
+        if flags[i]:
+            sig = float(getattr(ref, nm + "_err"))
+            assert abs(p[i] - float(getattr(ref, nm))) <= 1e-3 * sig, (nm, p[i], getattr(ref, nm))
+    assert r["red_chi2"][0] == pytest.approx(ref.red_chi2, rel=1e-8)
+    print("Newton-CG case %d: status %d, nfev %d (oracle %d)" % (
+        ic, int(r["status"][0]), int(r["nfev"][0]), ref.nfeval))
