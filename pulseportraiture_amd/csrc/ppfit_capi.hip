@@ -228,22 +228,25 @@ int resolve_timing(ppf_ctx* ctx) {
 
 // Template spectra for nrow rows of nbin (DC zeroed when zero_dc).
 int model_spectra(ppf_ctx* ctx, int nrow, int nbin, const double* model, int zero_dc, Buffer& buf,
-                  double2** M, double** pn) {
+                  double2** M, double** pn, double** M2 = nullptr) {
   int logN;
   if (int r = check_nbin(ctx, nbin, &logN)) return r;
   const int NHP = nharm_pad(nbin);
   const size_t mbytes = (size_t)nrow * NHP * sizeof(double2);
   const size_t pbytes = ((size_t)nrow * sizeof(double) + 255) & ~(size_t)255;
-  if (int r = ensure(ctx, buf, mbytes + pbytes)) return r;
+  const size_t m2bytes = M2 ? (size_t)nrow * NHP * sizeof(double) : 0;
+  if (int r = ensure(ctx, buf, mbytes + pbytes + m2bytes)) return r;
   *M = reinterpret_cast<double2*>(buf.p);
   *pn = reinterpret_cast<double*>(static_cast<char*>(buf.p) + mbytes);
+  double* m2p = nullptr;
+  if (M2) *M2 = m2p = reinterpret_cast<double*>(static_cast<char*>(buf.p) + mbytes + pbytes);
   const double2* tw;
   if (int r = twiddles(ctx, nbin, &tw)) return r;
   double2* Mp = *M;
   double* pp = *pn;
   return timed(ctx, PPF_K_MODEL_FFT, [&] {
     LOGN_SWITCH(logN, hipLaunchKernelGGL(k_model_spec<LG>, dim3(nrow), dim3(kBlock), 0,
-                                         ctx->stream, model, Mp, pp, NHP, zero_dc, tw));
+                                         ctx->stream, model, Mp, pp, NHP, zero_dc, tw, m2p));
   });
 }
 
@@ -372,7 +375,8 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   if (int r = twiddles(ctx, nbin, &tw)) return r;
   double2* M;
   double* pn;
-  if (int r = model_spectra(ctx, d->nmodel * nchan, nbin, d->model, 1, ctx->mspec, &M, &pn))
+  double* M2;
+  if (int r = model_spectra(ctx, d->nmodel * nchan, nbin, d->model, 1, ctx->mspec, &M, &pn, &M2))
     return r;
 
   // X, the cross-spectrum, is written once by k_data_xspec.  Phase-family
@@ -461,6 +465,7 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   fa.X = sa.X;
   fa.R = sa.R;
   fa.M = M;
+  fa.M2 = M2;
   fa.pn = pn;
   fa.model_idx = d->model_idx;
   fa.sig = sa.sig;

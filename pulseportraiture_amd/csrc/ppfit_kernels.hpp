@@ -82,6 +82,7 @@ struct FitArgs {
   const double2* X;          // chunk [c][nchan][NHP]
   const double2* R;          // chunk [c][NHP]
   const double2* M;          // [nmodel][nchan][NHP]
+  const double* M2;          // [nmodel][nchan][NHP] |M|^2 (scattering sweeps)
   const double* pn;          // [nmodel][nchan]
   const int* model_idx;      // [nsub] or null
   const double* sig;         // chunk [c][nchan]
@@ -424,7 +425,7 @@ struct ResidArgs {
 __global__ void k_twiddles(double2* tw, int nbin);
 template <int LOGN>
 __global__ void k_model_spec(const double* model, double2* M, double* pn, int NHP, int zero_dc,
-                             const double2* tw);
+                             const double2* tw, double* M2);
 template <int LOGN> __global__ void k_data_xspec(SpecArgs a);
 template <int LOGN> __global__ void k_phase_shift(PhaseShiftArgs a);
 template <int LOGN>

@@ -42,7 +42,8 @@ __global__ __launch_bounds__(kBlock) void k_model_spec(const double* __restrict_
                                                        double2* __restrict__ M,
                                                        double* __restrict__ pn, int NHP,
                                                        int zero_dc,
-                                                       const double2* __restrict__ tw) {
+                                                       const double2* __restrict__ tw,
+                                                       double* __restrict__ M2) {
   constexpr int N = 1 << LOGN;
   __shared__ double2 buf[N];
   __shared__ double red[kWaves];
@@ -58,6 +59,7 @@ __global__ __launch_bounds__(kBlock) void k_model_spec(const double* __restrict_
     if (k == 0 && zero_dc) x = cmk(0.0, 0.0);
     if (k >= 1 && k <= N) p += cabs2(x);
     out[k] = x;
+    if (M2) M2[(size_t)row * NHP + k] = cabs2(x);  // |M_k|^2 for the scattering sweeps
   }
   p = block_sum(p, red);
   if (threadIdx.x == 0 && pn) pn[row] = p;
@@ -672,7 +674,7 @@ __global__ __launch_bounds__(kBlock) void k_resid_chi2(ResidArgs a, const double
 // ---------------------------------------------------------------------------
 #define PPF_INST(L)                                                                          \
   template __global__ void k_model_spec<L>(const double*, double2*, double*, int, int,       \
-                                           const double2*);                                  \
+                                           const double2*, double*);                         \
   template __global__ void k_data_xspec<L>(SpecArgs);                                        \
   template __global__ void k_phase_shift<L>(PhaseShiftArgs);                                 \
   template __global__ void k_rotate_rows<L>(const double*, const double*, const double*,     \
