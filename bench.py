@@ -74,8 +74,9 @@ def parse():
                     help="subints the 1-core oracle fits (default per config; 0: skip)")
     ap.add_argument("--cpu-procs", type=int, default=16,
                     help="processes (one per core) of the all-core CPU baseline")
-    ap.add_argument("--cpu-seconds", type=float, default=8.0,
-                    help="approximate fit seconds per process of the all-core leg")
+    ap.add_argument("--cpu-seconds", type=float, default=24.0,
+                    help="approximate CPU work (core-seconds, summed over the processes) "
+                         "of the all-core leg")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP events")
     ap.add_argument("--host-stream", type=int, default=None,
                     help="also time host-resident (pinned) input streamed over PCIe in chunks "

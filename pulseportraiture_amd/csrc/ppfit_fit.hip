@@ -193,7 +193,7 @@ __device__ __forceinline__ double rcp_nr(double d) {
 __device__ __forceinline__ void cells_scat(const double2* __restrict__ Xr,
                                            const double* __restrict__ M2r, int J, int h,
                                            double phif, double taun, double* acc) {
-  constexpr int U = 2;  // 4 in flight: 256 VGPRs, one wave per SIMD, no faster (r01)
+  constexpr int U = 4;  // 4 in flight: 256 VGPRs, one wave per SIMD, no faster (r01)
   const double2 step = turn_phasor(8.0, phif);
   const double itau = 1.0 / taun;
   const double w0 = kTwoPi * taun;
