@@ -9,3 +9,7 @@ timeout -k 10 300 python -u bench.py --config scattering --steps 3 --warmup 1 --
 python -c "
 import json;d=json.loads(open('gpurun_out/r3d_bench_cfg3.log').read().strip().splitlines()[-1])
 print(d['value'], d['ms_per_step'], d['mean_nfev'], d['roofline']['frac'], {k: round(v,3) for k,v in d['roofline']['kernel_ms_per_step'].items()})"
+timeout -k 10 300 python -u tools/post_probe.py > gpurun_out/r3d_post.log 2>&1 || { echo "post probe failed"; tail -20 gpurun_out/r3d_post.log; exit 1; }
+tail -6 gpurun_out/r3d_post.log
+timeout -k 10 300 python -u tools/phase_probe.py 10000 > gpurun_out/r3d_phase.log 2>&1 || { echo "phase probe failed"; tail -20 gpurun_out/r3d_phase.log; exit 1; }
+tail -2 gpurun_out/r3d_phase.log
