@@ -188,6 +188,16 @@ int sync_event(ppf_ctx* ctx, size_t i, hipEvent_t* out) {
   return PPF_OK;
 }
 
+// the single-wave guess (k_guess_w) for the subints it covers; PPF_GUESS_WAVE=0
+// leaves every guess to k_guess (A/B timing)
+bool guess_wave_on() {
+  static const bool on = [] {
+    const char* e = getenv("PPF_GUESS_WAVE");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 // default pieces per chunk of the two-queue pipeline on the Taylor path
 // (PPF_PIPE overrides; 1 = one queue, the chunk as one launch per kernel)
 int pipe_default() {
@@ -460,6 +470,7 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   fa.guess_wrap = d->guess_wrap;
   fa.solver_flags = d->solver_flags;
   fa.method = d->method;
+  fa.guess_wave = guess_wave_on() ? 1 : 0;
   for (int i = 0; i < 5; ++i)
     for (int j = 0; j < 2; ++j) fa.bounds[i][j] = d->bounds ? d->bounds[2 * i + j] : NAN;
   fa.X = sa.X;
@@ -572,6 +583,8 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
         if (int r = sync_event(ctx, ev++, &prev_x)) return r;
         HIPCHK(ctx, hipEventRecord(prev_x, st));
         if (int r = timed_on(ctx, PPF_K_GUESS, st, [&] {
+              if (d->guess && fp.guess_wave)
+                hipLaunchKernelGGL(k_guess_w, dim3(n), dim3(64), 0, st, fp);
               hipLaunchKernelGGL(k_guess, dim3(n), dim3(kBlock), d->guess ? lds_guess : 0, st, fp);
             }))
           return r;
@@ -610,6 +623,8 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
         }))
       return r;
     if (int r = timed(ctx, PPF_K_GUESS, [&] {
+          if (d->guess && fa.guess_wave)
+            hipLaunchKernelGGL(k_guess_w, dim3(nc), dim3(64), 0, ctx->stream, fa);
           hipLaunchKernelGGL(k_guess, dim3(nc), dim3(kBlock), d->guess ? lds_guess : 0,
                              ctx->stream, fa);
         }))

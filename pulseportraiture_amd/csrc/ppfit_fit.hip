@@ -804,11 +804,306 @@ __device__ void guess_subint(const FitArgs& a, int c, int s, unsigned char* dyn,
   }
 }
 
+__device__ bool guess_wave_ok(const FitArgs& a, int s);  // below, with k_guess_w
+
 __global__ __launch_bounds__(kBlock) void k_guess(FitArgs a) {
   extern __shared__ __align__(16) unsigned char dyn[];
   __shared__ GuessShared gs;
   const int c = blockIdx.x, s = a.sub0 + c;
+  if (guess_wave_ok(a, s)) return;  // k_guess_w's subint
   guess_subint(a, c, s, dyn, gs);
+}
+
+// ---------------------------------------------------------------------------
+// k_guess_w: the get_TOAs guess of one subint per wave (64 threads) in the
+// common case -- every channel fitted (the guess template is Mmean), the
+// folded grid (lo, hi) = (-1/2, 1/2) with 2 <= Ns - 1 <= kBlock / 2 and
+// NH > 2 (Ns - 1), NH <= 17 * 64.  Lane l plays k_guess's threads l + 64 q
+// (q < 4): rm_k for k = l + 64 m (m < 17) lives in registers; every sum is
+// formed with k_guess's operations in its order (per virtual thread, then
+// the wave's DPP tree, then the four waves in order), and the grid argmin is
+// a total order, so st.x / st.init come out bitwise k_guess's.  k_guess
+// skips the subints taken here.  No block barrier, 17 complex registers
+// instead of a 16.5 KB LDS spectrum: many more subints in flight per CU.
+// ---------------------------------------------------------------------------
+constexpr int kGwM = 17;  // rm registers per lane: k = lane + 64 m
+
+__device__ bool guess_wave_ok(const FitArgs& a, int s) {
+  if (!a.guess_wave || !a.guess || !a.Mmean || (a.solver_flags & PPF_GUESS_DIRECT)) return false;
+  const int L = a.Ns - 1;
+  if (!(L >= 2 && L <= kBlock / 2 && a.NH > 2 * L && a.NH <= kGwM * 64)) return false;
+  if (a.mask)
+    for (int n = 0; n < a.nchan; ++n)
+      if (!a.mask[(size_t)s * a.nchan + n]) return false;
+  return true;
+}
+
+// rm_k = R_k conj(Mm_k B_k(tg)) exactly as guess_subint forms it (unmasked)
+__device__ __forceinline__ double2 guess_rm(const FitArgs& a, const double2* Rr,
+                                            const double2* Mm, double tg, int k) {
+  const int N = a.NH - 1;
+  const double2 r = Rr[k];
+  double2 mm = Mm[k];
+  if (k == N) mm.y = 0.0;
+  if (tg != 0.0) {
+    const double aa = kTwoPi * (double)k * tg;
+    const double id = 1.0 / fma(aa, aa, 1.0);
+    mm = cmul(mm, cmk(id, -aa * id));
+    if (k == N) mm.y = 0.0;
+  }
+  return cmulc(r, mm);
+}
+
+// The four virtual threads' wave sums of v_q, added in wave order: block_sum
+__device__ __forceinline__ double vsum4(const double (&v)[4]) {
+  double t = 0.0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) t += wave_sum(v[q]);
+  return t;
+}
+
+// block_eval_phase at phi over the registers (see there for the order)
+__device__ __forceinline__ double wave_eval_phase(const double2 (&rm)[kGwM], int NH, double phi,
+                                                  int lane) {
+  const double2 st = turn_phasor((double)kBlock, phi);
+  double acc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    double2 e = turn_phasor((double)(lane + 64 * q), phi);
+    double v = 0.0;
+#pragma unroll
+    for (int i = 0; i * 4 + q < kGwM; ++i) {
+      const int k = lane + 64 * (q + 4 * i);
+      if (k < NH) {
+        const double2 r = rm[q + 4 * i];
+        v = fma(r.x, e.x, v);
+        v = fma(-r.y, e.y, v);
+        e = cmul(e, st);
+      }
+    }
+    acc[q] = wave_sum(v);
+  }
+  return ((acc[0] + acc[1]) + acc[2]) + acc[3];
+}
+
+// row_eval_phase over rm recomputed from R and Mm (the direct-sum recheck)
+__device__ double row_eval_phase_g(const FitArgs& a, const double2* Rr, const double2* Mm,
+                                   double tg, int k0, int k1, double phi) {
+  const double2 z = turn_phasor(1.0, phi);
+  double acc = 0.0;
+  for (int kb = k0; kb < k1; kb += 64) {
+    double2 e = turn_phasor((double)kb, phi);
+    const int ke = min(kb + 64, k1);
+    for (int k = kb; k < ke; ++k) {
+      const double2 r = guess_rm(a, Rr, Mm, tg, k);
+      acc = fma(r.x, e.x, acc);
+      acc = fma(-r.y, e.y, acc);
+      e = cmul(e, z);
+    }
+  }
+  return acc;
+}
+
+__global__ __launch_bounds__(64) void k_guess_w(FitArgs a) {
+  __shared__ double2 fb[kBlock / 2], fw[kBlock / 2];
+  const int c = blockIdx.x, s = a.sub0 + c, lane = threadIdx.x;
+  if (!guess_wave_ok(a, s)) return;
+  const int nchan = a.nchan;
+  // fmean over the (all fitted) channels: block_sum of the threads' sums
+  double fv[4], cv[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    fv[q] = 0.0;
+    cv[q] = 0.0;
+    for (int n = lane + 64 * q; n < nchan; n += kBlock) {
+      fv[q] += a.freqs[(size_t)s * nchan + n];
+      cv[q] += 1.0;
+    }
+  }
+  const double fsum = vsum4(fv), cnt = vsum4(cv);
+  const double fmean = fsum / cnt;
+  SolveState& st = a.st[c];
+  if (lane == 0) {
+    for (int i = 0; i < 5; ++i) st.x[i] = a.init[(size_t)s * 5 + i];
+    for (int i = 0; i < 3; ++i) {
+      const double v = a.nu_fit[(size_t)s * 3 + i];
+      st.refs[i] = isnan(v) ? fmean : v;
+    }
+    st.nfev = 0;
+    st.status = -1;
+    st.slot = 0;
+    st.fun = NAN;
+    const double tl = a.log10_tau ? pow(10.0, st.x[3]) : st.x[3];
+    st.scat = (tl != 0.0) || a.flags[3];
+    st.scat_post = st.scat;
+    st.taylor = !st.scat && a.T != nullptr;
+    st.kit = 0;
+    st.sdone = 0;
+    st.phase = 0;
+    st.fin = 0;
+    st.mvalid = 0;
+    st.xslot = 0;
+    st.wslot = 0;
+    st.tr = 1.0;
+  }
+  const double2* Rr = a.R + (size_t)c * a.NHP;
+  const double tg = a.guess_tau ? a.guess_tau[s] : 0.0;
+  const int NH = a.NH;
+  const int midx = a.model_idx ? a.model_idx[s] : 0;
+  const double2* Mm = a.Mmean + (size_t)midx * a.NHP;
+  double2 rm[kGwM];
+  double pv[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int m = 0; m < kGwM; ++m) {
+    const int k = lane + 64 * m;
+    rm[m] = cmk(0.0, 0.0);
+    if (k < NH) {
+      rm[m] = guess_rm(a, Rr, Mm, tg, k);
+      if (k >= a.kc) pv[m & 3] += cabs2(Rr[k]);
+    }
+  }
+  const double pno = vsum4(pv);
+  const double noise = sqrt(pno / (double)a.nbin / (double)(NH - a.kc));
+  const double err2 = noise * noise * (0.5 * (double)a.nbin);
+  const double ie2 = 1.0 / err2;
+  // ---- folded brute force (guess_search, FOLD) ----
+  const int Ns = a.Ns, L = Ns - 1;
+  const double lo = -0.5, hi = 0.5;
+  const double step = (hi - lo) / (double)(Ns - 1);
+  for (int t = lane; t < L; t += 64) {
+    double2 b = cmk(0.0, 0.0);
+    for (int k = t; k < NH; k += L) {
+      const double2 r = guess_rm(a, Rr, Mm, tg, k);
+      b = (k & 1) ? csub(b, r) : cadd(b, r);
+    }
+    fb[t] = b;
+    double sn, cs;
+    sincospi(2.0 * (double)t / (double)L, &sn, &cs);
+    fw[t] = cmk(cs, sn);
+  }
+  __syncthreads();  // one wave: orders the LDS writes before the reads
+  const int jm = (L + 1) / 2;
+  double myf[2] = {NAN, NAN};
+  double bv = NAN;
+  int bi = 0x7fffffff;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int g = lane + 64 * u;
+    if (g < Ns) {
+      double part[2];
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const int j0 = half ? jm : 0, j1 = half ? L : jm;
+        double pt = 0.0;
+        int mi = (j0 * g) % L;
+        for (int j = j0; j < j1; ++j) {
+          const double2 b = fb[j], wv = fw[mi];
+          pt = fma(b.x, wv.x, pt);
+          pt = fma(-b.y, wv.y, pt);
+          mi += g;
+          if (mi >= L) mi -= L;
+        }
+        part[half] = pt;
+      }
+      const double f = -(part[0] + part[1]) * ie2;
+      myf[u] = f;
+      if (argmin_better(f, g, bv, bi)) { bv = f; bi = g; }
+    }
+  }
+  auto wave_argmin = [&](double& v, int& i) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const double ov = __shfl_xor(v, o);
+      const int oi = __shfl_xor(i, o);
+      if (argmin_better(ov, oi, v, i)) { v = ov; i = oi; }
+    }
+  };
+  wave_argmin(bv, bi);
+  // near tie on the folded grid: retake the grid by direct sums
+  bool near = false;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int g = lane + 64 * u;
+    const bool endpair = (bi == 0 && g == Ns - 1) || (bi == Ns - 1 && g == 0);
+    if (g < Ns && g != bi && !endpair && !(fabs(myf[u] - bv) > 1e-12 * fabs(bv))) near = true;
+  }
+  if (__any(near)) {
+    const int kmid = (NH + 1) / 2;
+    bv = NAN;
+    bi = 0x7fffffff;
+    for (int u = 0; u < 2; ++u) {
+      const int g = lane + 64 * u;
+      if (g < Ns) {
+        const double ph = (g == Ns - 1) ? hi : __dadd_rn(__dmul_rn((double)g, step), lo);
+        const double p0 = row_eval_phase_g(a, Rr, Mm, tg, 0, kmid, ph);
+        const double p1 = row_eval_phase_g(a, Rr, Mm, tg, kmid, NH, ph);
+        const double f = -(p0 + p1) * ie2;
+        if (argmin_better(f, g, bv, bi)) { bv = f; bi = g; }
+      }
+    }
+    wave_argmin(bv, bi);
+  }
+  const double x0 = (bi == Ns - 1) ? hi : __dadd_rn(__dmul_rn((double)bi, step), lo);
+  // ---- Nelder-Mead polish (guess_search) ----
+  const int maxfun = 200, maxiter = 200;
+  int fcalls = 0;
+  bool stop = false;
+  auto F = [&](double xv) -> double {
+    if (fcalls >= maxfun) { stop = true; return 0.0; }
+    ++fcalls;
+    return -wave_eval_phase(rm, NH, xv, lane) * ie2;
+  };
+  double s0 = x0;
+  double s1 = (s0 != 0.0) ? (1.0 + 0.05) * s0 : 0.00025;
+  double f0 = F(s0), f1 = F(s1);
+  if (f1 < f0) { double t = s0; s0 = s1; s1 = t; t = f0; f0 = f1; f1 = t; }
+  int it = 1;
+  while (fcalls < maxfun && it < maxiter) {
+    if (fabs(s1 - s0) <= 1e-4 && fabs(f0 - f1) <= 1e-4) break;
+    const double xbar = s0;
+    const double xr = __dsub_rn(__dmul_rn(2.0, xbar), s1);
+    const double fxr = F(xr);
+    if (stop) break;
+    bool shrink = false;
+    if (fxr < f0) {
+      const double xe = __dsub_rn(__dmul_rn(3.0, xbar), __dmul_rn(2.0, s1));
+      const double fxe = F(xe);
+      if (stop) break;
+      if (fxe < fxr) { s1 = xe; f1 = fxe; } else { s1 = xr; f1 = fxr; }
+    } else {
+      if (fxr < f1) {
+        const double xc = __dsub_rn(__dmul_rn(1.5, xbar), __dmul_rn(0.5, s1));
+        const double fxc = F(xc);
+        if (stop) break;
+        if (fxc <= fxr) { s1 = xc; f1 = fxc; } else shrink = true;
+      } else {
+        const double xcc = __dadd_rn(__dmul_rn(0.5, xbar), __dmul_rn(0.5, s1));
+        const double fxcc = F(xcc);
+        if (stop) break;
+        if (fxcc < f1) { s1 = xcc; f1 = fxcc; } else shrink = true;
+      }
+      if (shrink) {
+        s1 = __dadd_rn(s0, __dmul_rn(0.5, __dsub_rn(s1, s0)));
+        f1 = F(s1);
+        if (stop) break;
+      }
+    }
+    ++it;
+    if (f1 < f0) { double t = s0; s0 = s1; s1 = t; t = f0; f0 = f1; f1 = t; }
+  }
+  if (f1 < f0) { double t = s0; s0 = s1; s1 = t; }
+  if (lane == 0) {
+    double nug = a.guess_nu ? a.guess_nu[s] : NAN;
+    if (isnan(nug)) nug = fmean;
+    const double P = a.P[s];
+    const double DM = st.x[1];
+    double phi = s0;
+    // phase_transform(phi, DM_guess, nu_g, nu_fit_DM, P, mod), pplib.py:2609
+    phi = phi + (kDconst * DM * (1.0 / P) * (pow(st.refs[0], -2.0) - pow(nug, -2.0)));
+    if (a.guess_wrap) phi = wrap_half(phi);
+    st.x[0] = phi;
+    for (int i = 0; i < 5; ++i) { st.init[i] = st.x[i]; st.xc[0][i] = st.x[i]; }
+  }
 }
 
 // Mean of the DC-zeroed channel spectra of each template (unmasked guess

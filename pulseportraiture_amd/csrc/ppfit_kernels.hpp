@@ -79,6 +79,7 @@ struct FitArgs {
   int log10_tau, option, is_toa, guess, Ns, guess_wrap;
   int solver_flags;          // PPF_SOLVE_* / PPF_GUESS_* bits
   int method;                // PPF_METHOD_*
+  int guess_wave;            // k_guess_w takes the subints it covers (guess_wave_ok)
   const double2* X;          // chunk [c][nchan][NHP]
   const double2* R;          // chunk [c][NHP]
   const double2* M;          // [nmodel][nchan][NHP]
@@ -463,6 +464,7 @@ __global__ void k_selftest(int* fails);
 template <bool SCAT> __global__ void k_solve(FitArgs a);
 template <bool SCAT> __global__ void k_tnc(FitArgs a);
 template <bool SCAT> __global__ void k_ncg(FitArgs a);
+__global__ void k_guess_w(FitArgs a);
 template <bool SCAT> __global__ void k_post(FitArgs a);
 
 }  // namespace ppf
