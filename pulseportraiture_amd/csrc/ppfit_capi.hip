@@ -124,7 +124,7 @@ int twiddles(ppf_ctx* ctx, int nbin, const double2** out) {
 int moments_u() {
   static const int u = [] {
     const char* e = getenv("PPF_MOMENTS_U");
-    return (e && atoi(e) == 4) ? 4 : 8;
+    return (e && atoi(e) == 8) ? 8 : 4;
   }();
   return u;
 }

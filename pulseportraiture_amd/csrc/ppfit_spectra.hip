@@ -214,7 +214,9 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
       const double wgt = cm.y;
       double2 e = cmk(1.0, 0.0), estep = e, EN = e;
       if (a.guess) {
-        e = turn_phasor((double)lane, cm.x);
+        // the channel weight rides on the phasor chain (exact for the usual
+        // weight 1): w e_k = (w e_0) estep^k
+        e = cscale(turn_phasor((double)lane, cm.x), wgt);
         estep = turn_phasor(64.0, cm.x);
         EN = turn_phasor((double)N, cm.x);
       }
@@ -246,8 +248,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
           if (a.guess) {
             // e^{2 pi i (N-k) phi} = e^{2 pi i N phi} conj(e^{2 pi i k phi});
             // the pair's two slots are read and written by this lane only
-            const double2 tk = cscale(cmul(xk, e), wgt);
-            const double2 tn = cscale(cmul(xn, cmul(EN, cconj(e))), wgt);
+            const double2 tk = cmul(xk, e);
+            const double2 tn = cmul(xn, cmul(EN, cconj(e)));
             if (two) buf[bi(kn)] = tn;  // k = 0: the N slot
             buf[bi(k)] = tk;
           }

@@ -76,6 +76,13 @@ __device__ __forceinline__ void rs_swap(const double* v, double* out) {
 // ---------------------------------------------------------------------------
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
+// Steps (of 4 harmonics) between exact re-seeds of the phasor chains
+// (turn_phasor is a sincospi: re-seeded every block it cost more vector
+// issue than the chains); in between each chain advances by e^{2 pi i 8
+// phi_c} per step pair.  A multiple of every tile's U, so the 16- and
+// 8-channel tiles re-seed at the same harmonics (bitwise the same moments).
+constexpr int kMomReseedSteps = 8;
+
 // X rows: plain loads (the non-temporal hint measured slower here)
 __device__ __forceinline__ double2 xload(const double2* p) { return *p; }
 
@@ -111,7 +118,7 @@ __global__ void k_vpow(double2* vp, int N, int rows) {
 // A, with even and odd steps in separate accumulators (independent chains).
 // A lane rotates its own element and feeds it straight to the matrix core:
 // no cross-lane trade, no select.  Its two phasor chains (even / odd steps)
-// restart from turn_phasor every block.  The next block's X and power rows
+// restart from turn_phasor every kMomReseedSteps steps.  The next block's X and power rows
 // stream into each step's registers as soon as its MFMAs have issued, so U
 // steps of loads stay in flight with one register set.
 template <int U>
@@ -138,10 +145,13 @@ __device__ __forceinline__ void moment_tile16(const FitArgs& a, int c, int slot,
     xb[t] = (ok && k <= N) ? xload(Xr + k) : cmk(0.0, 0.0);
     pb[t] = vp[(size_t)t * 64];
   }
+  double2 e0 = cmk(1.0, 0.0), e1 = e0;
   for (int b = 0; b < nblk; ++b) {
     const bool more = b + 1 < nblk;
-    double2 e0 = turn_phasor((double)(4 * (b * U) + kk), phic);
-    double2 e1 = turn_phasor((double)(4 * (b * U + 1) + kk), phic);
+    if ((b * U) % kMomReseedSteps == 0) {  // exact phasors; the chains carry them between
+      e0 = turn_phasor((double)(4 * (b * U) + kk), phic);
+      e1 = turn_phasor((double)(4 * (b * U + 1) + kk), phic);
+    }
 #pragma unroll
     for (int u = 0; u < UP; ++u) {
       const double2 W0 = cmul(xb[2 * u], e0), W1 = cmul(xb[2 * u + 1], e1);
@@ -209,9 +219,10 @@ __device__ __forceinline__ void moment_tile8(const FitArgs& a, int c, int slot, 
     const int k = 4 * (2 * u + part) + kk;
     xb[u] = (ok && k <= N) ? Xr[k] : cmk(0.0, 0.0);
   }
+  double2 e = cmk(1.0, 0.0);
   for (int b = 0; b < nblk; ++b) {
     const bool more = b + 1 < nblk;
-    double2 e = turn_phasor((double)(4 * (b * U + part) + kk), phic);
+    if ((b * U) % kMomReseedSteps == 0) e = turn_phasor((double)(4 * (b * U + part) + kk), phic);
 #pragma unroll
     for (int u = 0; u < UP; ++u) {
       const double2 W = cmul(xb[u], e);
