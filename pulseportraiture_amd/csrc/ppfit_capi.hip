@@ -577,7 +577,7 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
         if (int r = timed_on(ctx, PPF_K_DATA_XSPEC, st, [&] {
               LOGN_SWITCH(logN, hipLaunchKernelGGL(k_data_xspec<LG>, dim3(n),
                                                    dim3(XspecCfg<LG>::WPB * 64),
-                                                   (size_t)nchan * sizeof(double2), st, sp));
+                                                   xspec_dyn_lds(nchan), st, sp));
             }))
           return r;
         if (int r = sync_event(ctx, ev++, &prev_x)) return r;
@@ -618,7 +618,7 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
     sa.sub0 = (int)s0;
     fa.sub0 = (int)s0;
     if (int r = timed(ctx, PPF_K_DATA_XSPEC, [&] {
-          LOGN_SWITCH(logN, hipLaunchKernelGGL(k_data_xspec<LG>, dim3(nc), dim3(XspecCfg<LG>::WPB * 64), (size_t)nchan * sizeof(double2),
+          LOGN_SWITCH(logN, hipLaunchKernelGGL(k_data_xspec<LG>, dim3(nc), dim3(XspecCfg<LG>::WPB * 64), xspec_dyn_lds(nchan),
                                                ctx->stream, sa));
         }))
       return r;

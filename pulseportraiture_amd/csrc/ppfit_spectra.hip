@@ -95,6 +95,12 @@ struct XspecCfg {
   static constexpr int NRQ = RREG ? (N + 1 + WPB * 64 - 1) / (WPB * 64) : 1;  // R slots/thread
 };
 
+// dynamic LDS of k_data_xspec: per-channel (phi_g, weight) then one
+// active flag per channel (the group loop reads LDS, not the mask in HBM)
+inline size_t xspec_dyn_lds(int nchan) {
+  return (size_t)nchan * sizeof(double2) + (((size_t)nchan + 15) & ~(size_t)15);
+}
+
 template <int LOGN>
 __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
   using Cfg = XspecCfg<LOGN>;
@@ -116,19 +122,22 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
   __shared__ int s_act[WPB];
   extern __shared__ __align__(16) unsigned char dyn[];
   double2* cmeta = reinterpret_cast<double2*>(dyn);  // (phi_g, weight or NaN if masked)
+  uint8_t* cact = dyn + (size_t)a.nchan * sizeof(double2);  // fitted channel flags
   const int c = blockIdx.x;
   const int s = a.sub0 + c;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: row pointers in SGPRs
   const int nchan = a.nchan;
   const int midx = a.model_idx ? a.model_idx[s] : 0;
   const double* fr = a.freqs + (size_t)s * nchan;
   const uint8_t* mask = a.mask ? a.mask + (size_t)s * nchan : nullptr;
   const double* drow0 = a.data + (size_t)s * nchan * (2 * N);
   double2* buf = bufs[w];
-  auto active = [&](int q) { return q < nchan && (!mask || mask[q]); };
+  auto active_g = [&](int q) { return q < nchan && (!mask || mask[q]); };
+  auto active = [&](int q) { return q < nchan && cact[q]; };  // after the cmeta barrier
 
   WaveRow<LOGN> row;
-  bool have = active(w);  // the registers hold (or are loading) this wave's next row
+  bool have = active_g(w);  // the registers hold (or are loading) this wave's next row
   if (have) row.load(drow0 + (size_t)w * 2 * N, lane);  // first row in flight
   if constexpr (REGFFT) ftw[0].fill(a.tw, tid, nthr);
   else fill_pass_tw<LOGN>(twl, a.tw, tid, nthr);
@@ -160,6 +169,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
       const bool ok = !mask || mask[q];
       const double wq = a.weights ? a.weights[(size_t)s * nchan + q] : 1.0;
       cmeta[q] = cmk(Dfac * (1.0 / (fr[q] * fr[q]) - nug2), ok ? wq : NAN);
+      cact[q] = ok;
     }
   }
   double2 rq[Cfg::NRQ];  // R harmonics owned by this thread (RREG)
@@ -188,9 +198,12 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
     const double2* Mr = a.M + ((size_t)midx * nchan + (act ? n : 0)) * a.NHP;
     // rolling prefetch two pair iterations deep: (m0k, m0n) for iteration i,
     // (m1k, m1n) for i + 1; the first two are issued before the FFT
+    // unpredicated (k clamped to N/2 past the end): no merge with the old
+    // value, so an unrolled loop renames the prefetch registers, no copies
     auto mload = [&](int i, double2& mk, double2& mn) {
-      const int k = lane + 64 * i;
-      if (i < NPI && k <= N / 2) { mk = Mr[k]; mn = Mr[N - k]; }
+      const int k = min(lane + 64 * i, N / 2);
+      mk = Mr[k];
+      mn = Mr[N - k];
     };
     double2 m0k = cmk(0.0, 0.0), m0n = m0k, m1k = m0k, m1n = m0k;
     if (act) {
@@ -223,20 +236,22 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
       double2* Xr = wx ? a.X + ((size_t)c * nchan + n) * a.NHP : nullptr;
       double pn = 0.0, pd = 0.0;
       double2 tw = w0;
-#pragma unroll 1
-      for (int i = 0; i < NPI; ++i) {
+      // pair iteration i: k = lane + 64 i.  Every iteration but the last has
+      // k < N/2 on every lane (a pair of two distinct harmonics); the last
+      // holds k = N/2 (its own partner) on lane 0 only.  The full iterations
+      // are branch-free so the stores and template loads keep a fixed count.
+      // mk / mn hold iteration i's template harmonics and take iteration
+      // i + 2's once used: the two register pairs alternate (no copies)
+      auto pair = [&](int i, auto fullc, double2& mk, double2& mn) {
+        constexpr bool FULL = decltype(fullc)::value;
         const int k = lane + 64 * i;
         if (i > 0) { tw = cmul(tw, wstep); e = cmul(e, estep); }
-        const double2 mk = m0k, mn = m0n;
-        m0k = m1k;
-        m0n = m1n;
-        mload(i + 2, m1k, m1n);
-        if (k <= N / 2) {
+        if (FULL || k <= N / 2) {
           double2 xk, xn;
           rfft_pair_v(buf[bi(k)], buf[bi((N - k) & (N - 1))], tw, xk, xn);
           const int kn = N - k;
           const double p2k = cabs2(xk), p2n = cabs2(xn);
-          const bool two = k < N / 2;  // k = N/2 is its own partner
+          const bool two = FULL || k < N / 2;  // k = N/2 is its own partner
           if (k >= a.kc) pn += p2k;
           if (two && kn >= a.kc) pn += p2n;
           if (k >= 1) pd += p2k;
@@ -254,6 +269,20 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
             buf[bi(k)] = tk;
           }
         }
+        if (FULL) mload(i + 2, mk, mn);
+      };
+      static_assert(64 * (NPI - 1) <= N / 2 && 64 * (NPI - 1) + 63 >= N / 2, "pair split");
+      constexpr int NFULL2 = (NPI - 1) & ~1;
+#pragma unroll 1
+      for (int i = 0; i < NFULL2; i += 2) {
+        pair(i, std::true_type{}, m0k, m0n);
+        pair(i + 1, std::true_type{}, m1k, m1n);
+      }
+      if constexpr (NFULL2 < NPI - 1) {
+        pair(NPI - 2, std::true_type{}, m0k, m0n);
+        pair(NPI - 1, std::false_type{}, m1k, m1n);
+      } else {
+        pair(NPI - 1, std::false_type{}, m0k, m0n);
       }
       if (wx)
       for (int k = NH + lane; k < a.NHP; k += 64) Xr[k] = cmk(0.0, 0.0);
