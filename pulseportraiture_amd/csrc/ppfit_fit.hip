@@ -148,24 +148,23 @@ __device__ __forceinline__ void cells_phase(const double2* __restrict__ Xr, int 
   const double2 zero = cmk(0.0, 0.0);
   double2 e = cmk(1.0, 0.0);
   double a0 = 0.0, a1 = 0.0, a2 = 0.0;
-  double2 nx[kPipe];
+  // the register-set alternation of cells_scat (no copies of in-flight loads)
+  constexpr int U = kPipe;
+  const int Jpad = (J + U - 1) / U * U;
+  double2 xa[U], xb[U];
+  auto load = [&](int jb, double2 (&x)[U]) {
 #pragma unroll
-  for (int u = 0; u < kPipe; ++u) nx[u] = u < J ? Xr[h + 8 * u] : zero;
-  for (int j0 = 0; j0 < J; j0 += kPipe) {
-    double2 cx[kPipe];
+    for (int u = 0; u < U; ++u) x[u] = Xr[h + 8 * min(jb + u, J - 1)];
+  };
+  auto consume = [&](int jb, const double2 (&xs)[U]) {
 #pragma unroll
-    for (int u = 0; u < kPipe; ++u) cx[u] = nx[u];
-#pragma unroll
-    for (int u = 0; u < kPipe; ++u) {
-      const int j = j0 + kPipe + u;
-      nx[u] = j < J ? Xr[h + 8 * j] : zero;
-    }
-#pragma unroll
-    for (int u = 0; u < kPipe; ++u) {
-      const int k = h + 8 * (j0 + u);
-      if (u == 0 && (j0 & 31) == 0) e = turn_phasor((double)k, phif);
+    for (int u = 0; u < U; ++u) {
+      const int jj = jb + u;
+      if (jj >= Jpad) break;
+      const int k = h + 8 * jj;
+      if ((jj & 31) == 0) e = turn_phasor((double)k, phif);
       else e = cmul(e, step);
-      const double2 x = cx[u];
+      const double2 x = jj < J ? xs[u] : zero;
       const double wr = fma(x.x, e.x, -x.y * e.y);
       const double wi = fma(x.x, e.y, x.y * e.x);
       const double kd = (double)k;
@@ -173,6 +172,14 @@ __device__ __forceinline__ void cells_phase(const double2* __restrict__ Xr, int 
       a1 = fma(kd, wi, a1);
       a2 = fma(kd * kd, wr, a2);
     }
+  };
+  load(0, xa);
+  load(U, xb);
+  for (int jb = 0; jb < Jpad; jb += 2 * U) {
+    consume(jb, xa);
+    load(jb + 2 * U, xa);
+    consume(jb + U, xb);
+    load(jb + 3 * U, xb);
   }
   acc[0] = a0; acc[1] = a1; acc[2] = a2;
   for (int i = 3; i < NACC; ++i) acc[i] = 0.0;
@@ -203,31 +210,31 @@ __device__ __forceinline__ void cells_scat(const double2* __restrict__ Xr,
   double2 e = cmk(1.0, 0.0);
   double a[NACC];
   for (int i = 0; i < NACC; ++i) a[i] = 0.0;
-  double2 nx[U];
-  double nm[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    nx[u] = u < J ? Xr[h + 8 * u] : zero;
-    nm[u] = u < J ? M2r[h + 8 * u] : 0.0;
-  }
-  for (int j0 = 0; j0 < J; j0 += U) {
-    double2 cx[U];
-    double cm[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) { cx[u] = nx[u]; cm[u] = nm[u]; }
+  // cells j < Jpad (U-aligned; j >= J are zero cells, as before); two register
+  // sets of U cells alternate, each reloaded (clamped, unpredicated) right
+  // after it is consumed, so the loop carries no copies of in-flight loads
+  const int Jpad = (J + U - 1) / U * U;
+  double2 xa[U], xb[U];
+  double ma[U], mb[U];
+  auto load = [&](int jb, double2 (&x)[U], double (&m)[U]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int j = j0 + U + u;
-      nx[u] = j < J ? Xr[h + 8 * j] : zero;
-      nm[u] = j < J ? M2r[h + 8 * j] : 0.0;
+      const int j = min(jb + u, J - 1);
+      x[u] = Xr[h + 8 * j];
+      m[u] = M2r[h + 8 * j];
     }
+  };
+  auto consume = [&](int jb, const double2 (&xs)[U], const double (&ms)[U]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int k = h + 8 * (j0 + u);
-      if (u == 0 && (j0 & 31) == 0) e = turn_phasor((double)k, phif);
+      const int jj = jb + u;
+      if (jj >= Jpad) break;
+      const int k = h + 8 * jj;
+      if ((jj & 31) == 0) e = turn_phasor((double)k, phif);
       else e = cmul(e, step);
-      const double2 x = cx[u];
-      const double m2 = cm[u];
+      const bool ok = jj < J;
+      const double2 x = ok ? xs[u] : zero;
+      const double m2 = ok ? ms[u] : 0.0;
       const double2 W = cmul(x, e);
       const double kd = (double)k;
       const double aa = w0 * kd;
@@ -250,6 +257,15 @@ __device__ __forceinline__ void cells_scat(const double2* __restrict__ Xr,
       a[8] = fma(cabs2(f), m2, a[8]);
       a[9] = fma(fma(B.x, g1.x, B.y * g1.y), m2, a[9]);
     }
+  };
+  static_assert(32 % U == 0, "phasor re-seed every 32 cells");
+  load(0, xa, ma);
+  load(U, xb, mb);
+  for (int jb = 0; jb < Jpad; jb += 2 * U) {
+    consume(jb, xa, ma);
+    load(jb + 2 * U, xa, ma);
+    consume(jb + U, xb, mb);
+    load(jb + 3 * U, xb, mb);
   }
   for (int i = 0; i < NACC; ++i) acc[i] = a[i];
 }
