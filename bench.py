@@ -47,7 +47,7 @@ FP64_PEAK_TFLOPS = 78.6  # AMD MI355X spec, fp64 vector = fp64 matrix (not in th
 # passes over this same bench (tools/profile_r1.sh + tools/pmc_summary.py).
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
 KERNEL_SYMBOL = {"solve": "k_solve<false>", "data_xspec": "k_data_xspec<10>",
-                 "post": "k_post<false>", "guess": "k_guess", "moments": "k_moments<8>",
+                 "post": "k_post<false>", "guess": "k_guess_w", "moments": "k_moments<4>",
                  "fit_taylor": "k_fit_taylor"}
 
 
