@@ -138,23 +138,27 @@ __device__ __forceinline__ void moment_tile16(const FitArgs& a, int c, int slot,
   // re (d) and im (g) parts; moments 0-15 / 16-31; even / odd steps
   f64x4 d0 = {0.0, 0.0, 0.0, 0.0}, d1 = d0, d2 = d0, d3 = d0;
   f64x4 g0 = d0, g1 = d0, g2 = d0, g3 = d0;
+  // loads are unpredicated (X index clamped to N; the power table is padded
+  // past the last block); cells k > N and idle lanes are zeroed at use
   double2 xb[U], pb[U];
 #pragma unroll
   for (int t = 0; t < U; ++t) {
-    const int k = 4 * t + kk;
-    xb[t] = (ok && k <= N) ? xload(Xr + k) : cmk(0.0, 0.0);
+    xb[t] = xload(Xr + min(4 * t + kk, N));
     pb[t] = vp[(size_t)t * 64];
   }
+  auto xcell = [&](int t, const double2& x) {
+    return (ok && 4 * t + kk <= N) ? x : cmk(0.0, 0.0);
+  };
   double2 e0 = cmk(1.0, 0.0), e1 = e0;
   for (int b = 0; b < nblk; ++b) {
-    const bool more = b + 1 < nblk;
     if ((b * U) % kMomReseedSteps == 0) {  // exact phasors; the chains carry them between
       e0 = turn_phasor((double)(4 * (b * U) + kk), phic);
       e1 = turn_phasor((double)(4 * (b * U + 1) + kk), phic);
     }
 #pragma unroll
     for (int u = 0; u < UP; ++u) {
-      const double2 W0 = cmul(xb[2 * u], e0), W1 = cmul(xb[2 * u + 1], e1);
+      const double2 W0 = cmul(xcell(b * U + 2 * u, xb[2 * u]), e0);
+      const double2 W1 = cmul(xcell(b * U + 2 * u + 1, xb[2 * u + 1]), e1);
       const double2 p0 = pb[2 * u], p1 = pb[2 * u + 1];
       d0 = __builtin_amdgcn_mfma_f64_16x16x4f64(p0.x, W0.x, d0, 0, 0, 0);
       d1 = __builtin_amdgcn_mfma_f64_16x16x4f64(p0.y, W0.x, d1, 0, 0, 0);
@@ -170,9 +174,8 @@ __device__ __forceinline__ void moment_tile16(const FitArgs& a, int c, int slot,
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int t = 2 * u + h;
-        const int k = 4 * ((b + 1) * U + t) + kk;
-        xb[t] = (more && ok && k <= N) ? xload(Xr + k) : cmk(0.0, 0.0);
-        if (more) pb[t] = vp[(size_t)((b + 1) * U + t) * 64];
+        xb[t] = xload(Xr + min(4 * ((b + 1) * U + t) + kk, N));
+        pb[t] = vp[(size_t)((b + 1) * U + t) * 64];
       }
     }
   }
