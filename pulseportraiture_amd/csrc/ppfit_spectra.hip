@@ -196,10 +196,11 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
     // template harmonics k and N - k of this row, in flight during the FFT
     // (M is shared by every subint: L2-resident)
     const double2* Mr = a.M + ((size_t)midx * nchan + (act ? n : 0)) * a.NHP;
-    // rolling prefetch two pair iterations deep: (m0k, m0n) for iteration i,
-    // (m1k, m1n) for i + 1; the first two are issued before the FFT
-    // unpredicated (k clamped to N/2 past the end): no merge with the old
-    // value, so an unrolled loop renames the prefetch registers, no copies
+    // prefetch two pair iterations deep: (m0k, m0n) serve the even iterations
+    // and (m1k, m1n) the odd ones, each reloaded for iteration i + 2 once
+    // iteration i has used it; the first two are issued before the FFT.
+    // Unpredicated (k clamped to N/2 past the end): no merge with the old
+    // value, so the registers are reloaded in place, no copies
     auto mload = [&](int i, double2& mk, double2& mn) {
       const int k = min(lane + 64 * i, N / 2);
       mk = Mr[k];
