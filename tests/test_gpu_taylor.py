@@ -78,7 +78,7 @@ def _assert_close(t, e, flags, tol=1e-3):
     np.testing.assert_allclose(t["scale_errs"], e["scale_errs"], rtol=1e-7, atol=1e-12)
 
 
-@pytest.mark.parametrize("nbin,nchan", [(64, 4), (256, 16), (1024, 33), (2048, 64),
+@pytest.mark.parametrize("nbin,nchan", [(64, 4), (128, 8), (256, 16), (1024, 33), (2048, 64),
                                         (4096, 8), (8192, 4)])
 def test_taylor_matches_exact_phase_dm(eng, nbin, nchan):
     w = synth.make_workload(6, nchan, nbin, seed=100 + nbin)
