@@ -276,6 +276,19 @@ int ppf_unpack_subints(ppf_ctx* ctx, int32_t nsub, int32_t npol, int32_t nchan, 
                        int32_t raw_type, const void* raw, const double* scl, const double* offs,
                        int32_t pmode, double* out);
 
+/* remove_baseline in place (load_data's arch.remove_baseline(),
+ * pplib.py:2691; PSRCHIVE Integration::remove_baseline with its default
+ * estimator): per subint s the total-intensity profile
+ *   t[j] = sum_{n: w[s][n] != 0} w[s][n] sum_{p < ntot} data[s][p][n][j]
+ * gives the off-pulse window [j0, j0 + width) (circular) of smallest sum,
+ * first on ties; every profile data[s][p][n] then has its mean over that
+ * window subtracted.  data [nsub][npol][nchan][nbin] (nbin <= 8192),
+ * weights [nsub][nchan]; window [nsub] receives j0 (NULL: not written).
+ * Callers pass width = floor(0.15 nbin), PSRCHIVE's default duty cycle.   */
+int ppf_remove_baseline(ppf_ctx* ctx, int32_t nsub, int32_t npol, int32_t nchan, int32_t nbin,
+                        int32_t ntot, int32_t width, double* data, const double* weights,
+                        int32_t* window);
+
 /* out[r] = irfft(rfft(in[r]) e^{2 pi i k phase[r]} / (1 + 2 pi i k tau[r]))
  * (rotate_portrait_full of a scattered template, pptoas.py:1389-1397);
  * tau NULL = no scattering.                                              */

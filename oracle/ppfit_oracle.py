@@ -110,6 +110,31 @@ def rotate_data(data, phase=0.0, DM=0.0, Ps=None, freqs=None, nu_ref=np.inf):
     return out.reshape(data.shape) if ndim in (1, 2) else out
 
 
+def remove_baseline(subints, weights, ntot=1, duty=0.15):
+    """arch.remove_baseline() as load_data calls it (pplib.py:2691), restated
+    from PSRCHIVE's documented default (Integration::remove_baseline with the
+    BaselineWindow estimator, duty cycle 0.15): per subint, the off-pulse
+    window is the circular run of floor(duty * nbin) bins with the smallest
+    sum of the total-intensity profile (weighted frequency sum of the first
+    ntot polarisations; first window on ties), and every profile has its mean
+    over that window subtracted.  PARITY UNPINNED: PSRCHIVE is not in this
+    image and the reference ships no archives.  Returns (out, window starts)."""
+    d = np.array(subints, dtype=float)
+    nsub, npol, nchan, nbin = d.shape
+    width = max(1, int(duty * nbin))
+    w = np.asarray(weights, dtype=float)
+    starts = np.zeros(nsub, dtype=int)
+    for s in range(nsub):
+        on = w[s] != 0.0
+        t = np.einsum("n,nj->j", w[s][on], d[s, :ntot][:, on].sum(axis=0))
+        box = np.array([t[(j + np.arange(width)) % nbin].sum() for j in range(nbin)])
+        j0 = int(np.argmin(box))
+        idx = (j0 + np.arange(width)) % nbin
+        d[s] -= d[s][..., idx].mean(axis=-1)[..., None]
+        starts[s] = j0
+    return d, starts
+
+
 def phase_shifts(phi, DM, GM, freqs, nu_DM=np.inf, nu_GM=np.inf, P=None):
     """Per-channel delay [rot], pptoaslib.py:181-214 (mod=False)."""
     if P is None:

@@ -104,6 +104,9 @@ EXPORTS = {
                                        ctypes.c_int),
     "ppf_tscrunch": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                       ctypes.c_int32, _dp, _dp, _dp, _dp], ctypes.c_int),
+    "ppf_remove_baseline": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                             ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _dp, _dp, _dp],
+                            ctypes.c_int),
     "ppf_synth_portraits": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
                              ctypes.c_int32, _dp, _dp, ctypes.c_double,
                              ctypes.c_uint64, ctypes.c_int64, _dp], ctypes.c_int),

@@ -7,21 +7,42 @@ DataBunches with the keys of pplib.py:2809-2819 registered under a name, or
 as ``.npz`` archives written by ``save_archive``.  Anything else raises
 RuntimeError, which the drivers treat exactly like a failed PSRCHIVE load
 (skip the archive, pptoas.py:271).
+
+Loading is split in two so a rank reads only the subints it fits
+(pptoas.py:246,343 sharded): ``open_archive`` returns the metadata (every
+load_data key but ``subints``) and a reader of subint ranges; ``load_data``
+is the two together.  The processing load_data asks PSRCHIVE for runs on the
+device in the reference's order (pplib.py:2686-2700): ``dedisperse`` /
+``dededisperse`` (per-channel rotation by the stored DM about the archive
+centre frequency, ppf_rotate_rows), ``rm_baseline`` (ppf_remove_baseline),
+then ``tscrunch`` (ppf_tscrunch).  A registered bunch or .npz is a load_data
+result: its ``dmc`` says whether it is dedispersed and its baseline counts as
+removed unless it says ``baseline_removed=False``.
 """
 import os
 
 import numpy as np
 
-from .mjd import MJD
-from .pplib import DataBunch, get_bin_centers
+from .mjd import MJD, epoch_parts
+from .pplib import DataBunch, Dconst, get_bin_centers
 
 _registry = {}
 
 REQUIRED = ["subints", "freqs", "Ps", "epochs"]
+DUTY_CYCLE = 0.15  # PSRCHIVE's default baseline duty cycle (Profile::default_duty_cycle)
+
+
+def _is_tensor(x):
+    try:
+        import torch
+    except ImportError:  # pragma: no cover
+        return False
+    return isinstance(x, torch.Tensor)
 
 
 def register_archive(name, bunch):
-    """Make an in-memory archive loadable under ``name``."""
+    """Make an in-memory archive loadable under ``name``.  ``subints`` may be
+    a numpy array or a float64 device tensor (kept on the device)."""
     _registry[name] = normalize(bunch, name)
     return name
 
@@ -30,36 +51,60 @@ def unregister_archive(name):
     _registry.pop(name, None)
 
 
-def normalize(b, name="archive"):
-    """Fill the load_data keys the drivers use from the minimal set."""
+def _ok_ichans(wn):
+    """[np.compress(wn[i], range(nchan)) for i] (pplib.py:2757-2758): rows with
+    every channel on share one index array."""
+    nsub, nchan = wn.shape
+    full = np.arange(nchan)
+    allok = wn.all(axis=1)
+    return [full if a else np.flatnonzero(r) for a, r in zip(allok.tolist(), wn)]
+
+
+def normalize(b, name="archive", subints=True):
+    """Fill the load_data keys the drivers use from the minimal set.
+
+    masks (pplib.py:2759-2761) is a read-only broadcast view of the
+    per-channel weight flags, not an [nsub, npol, nchan, nbin] array."""
     b = DataBunch(**dict(b))
-    subints = np.asarray(b["subints"], dtype=np.float64)
-    if subints.ndim == 3:
-        subints = subints[:, None]
-    nsub, npol, nchan, nbin = subints.shape
-    b.subints = subints
+    if subints:
+        sub = b["subints"]
+        if _is_tensor(sub):
+            import torch
+            sub = sub.to(torch.float64)
+            if sub.dim() == 3:
+                sub = sub.unsqueeze(1)
+            sub = sub.contiguous()
+        else:
+            sub = np.asarray(sub, dtype=np.float64)
+            if sub.ndim == 3:
+                sub = sub[:, None]
+        b.subints = sub
+        nsub, npol, nchan, nbin = tuple(sub.shape)
+    else:
+        nsub, npol, nchan, nbin = b.nsub, b.npol, b.nchan, b.nbin
     b.setdefault("filename", name)
-    b.setdefault("nsub", nsub)
-    b.setdefault("npol", npol)
-    b.setdefault("nchan", nchan)
-    b.setdefault("nbin", nbin)
+    b.nsub, b.npol, b.nchan, b.nbin = nsub, npol, nchan, nbin
     freqs = np.asarray(b["freqs"], dtype=np.float64)
     b.freqs = np.tile(freqs, (nsub, 1)) if freqs.ndim == 1 else freqs
     b.Ps = np.asarray(b["Ps"], dtype=np.float64) * np.ones(nsub)
     ep = b["epochs"]
     b.epochs = [e if isinstance(e, MJD) else MJD(*e) if np.ndim(e) else MJD(e) for e in ep]
+    b.epoch_parts = epoch_parts(b.epochs)  # (days, secs, fracsec) arrays of the epochs
     w = np.asarray(b.get("weights", np.ones((nsub, nchan))), dtype=np.float64)
     b.weights = w
-    wn = np.where(w == 0.0, 0.0, 1.0)
-    b.setdefault("ok_isubs", np.compress(wn.mean(axis=1), range(nsub)))
-    b.setdefault("ok_ichans", [np.compress(wn[i], range(nchan)) for i in range(nsub)])
-    b.setdefault("masks", np.einsum("j,ikl", np.ones(npol), np.einsum("ij,k", wn, np.ones(nbin))))
+    wn = w != 0.0
+    b.setdefault("ok_isubs", np.flatnonzero(wn.any(axis=1)))
+    b.setdefault("ok_ichans", _ok_ichans(wn))
+    if "masks" not in b:
+        b.masks = np.broadcast_to(wn.astype(np.float64)[:, None, :, None],
+                                  (nsub, npol, nchan, nbin))
     b.setdefault("phases", get_bin_centers(nbin))
     b.setdefault("SNRs", np.ones((nsub, npol, nchan)))
     b.setdefault("doppler_factors", np.ones(nsub))
     b.setdefault("parallactic_angles", np.zeros(nsub))
     b.setdefault("DM", 0.0)
     b.setdefault("dmc", 0)
+    b.setdefault("baseline_removed", True)
     b.setdefault("backend", "unknown")
     b.setdefault("frontend", "unknown")
     b.setdefault("backend_delay", 0.0)
@@ -78,32 +123,76 @@ def normalize(b, name="archive"):
     return b
 
 
-def tscrunch(b, period_at=None):
-    """arch.tscrunch() as load_data applies it (pplib.py:2700) to a normalised
-    archive: one subint whose profiles are the weight-averaged profiles of
-    all subints (fold-mode subints share the predictor's phase, so they add
-    without rotation), weights summed per channel (ppf_tscrunch, on the
-    device).  Epoch: the duration-weighted mean epoch (the middle of the span
-    for contiguous equal subints); duration: the sum; period: period_at(epoch
-    in days) when the archive has a predictor (PSRFITS POLYCO), else the
-    duration-weighted mean; Doppler factor, parallactic angle and SNRs: the
-    (duration-weighted) means.  PSRCHIVE recomputes some of these from the
-    ephemeris and its own estimators, which this build does not have: parity
-    with PSRCHIVE is unpinned (DESIGN.md)."""
-    from .engine import get_engine
-    b = normalize(b, b.get("filename", "archive"))
-    if b.nsub == 1:
-        return b
-    sub, ws = get_engine().tscrunch(b.subints, b.weights)
+# ---------------------------------------------------------------------------
+# sources: metadata + a reader of raw subint ranges
+# ---------------------------------------------------------------------------
+class _Registered:
+    def __init__(self, name):
+        self.base = _registry[name]
+
+    def meta(self):
+        return DataBunch(**{k: v for k, v in self.base.items() if k != "subints"})
+
+    def read(self, lo, hi):
+        return self.base.subints[lo:hi]
+
+
+class _Npz:
+    def __init__(self, path):
+        self.z = np.load(path, allow_pickle=False)
+        self.path = path
+
+    def meta(self):
+        z = self.z
+        b = {k: z[k] for k in z.files if k not in ("subints", "epochs") and
+             not k.startswith("meta_")}
+        b["epochs"] = [MJD(int(d), int(s), f) for d, s, f in z["epochs"]]
+        for k in z.files:
+            if k.startswith("meta_"):
+                v = z[k]
+                b[k[5:]] = v.item() if v.ndim == 0 else v
+        if "dmc" in b:
+            b["dmc"] = int(b["dmc"])
+        sh = z["subints"].shape  # a .npy header read; the data load is in read()
+        sh = sh if len(sh) == 4 else (sh[0], 1) + tuple(sh[1:])
+        b.update(nsub=sh[0], npol=sh[1], nchan=sh[2], nbin=sh[3])
+        return normalize(b, self.path, subints=False)
+
+    def read(self, lo, hi):
+        s = self.z["subints"]
+        return (s if s.ndim == 4 else s[:, None])[lo:hi]
+
+
+def _source(filename, pscrunch):
+    if filename in _registry:
+        return _Registered(filename)
+    if isinstance(filename, str) and is_fits(filename):
+        from .psrfits import PSRFITSSource
+        return PSRFITSSource(filename, pscrunch=pscrunch)
+    if isinstance(filename, str) and os.path.exists(filename) and filename.endswith(".npz"):
+        return _Npz(filename)
+    raise RuntimeError("Cannot load_data(%s): not a registered, .npz or PSRFITS archive "
+                       "(other PSRCHIVE formats need PSRCHIVE)" % filename)
+
+
+def _tscrunch_meta(b, period_at=None):
+    """Metadata of arch.tscrunch() (pplib.py:2700): one subint, weights summed
+    per channel; epoch the duration-weighted mean epoch (the middle of the
+    span for contiguous equal subints); duration the sum; period period_at
+    (epoch in days) when the archive has a predictor (PSRFITS POLYCO), else the
+    duration-weighted mean; Doppler factor, parallactic angle: the
+    (duration-weighted) means; SNRs added in quadrature.  PSRCHIVE recomputes
+    some of these from the ephemeris and its own estimators, which this build
+    does not have: parity with PSRCHIVE is unpinned (DESIGN.md)."""
     dur = np.asarray(b.subtimes, dtype=np.float64)
     wt = dur / dur.sum() if dur.sum() > 0 else np.full(b.nsub, 1.0 / b.nsub)
     e0 = b.epochs[0]
     offs = np.array([(e.days - e0.days) * 86400.0 + (e.secs - e0.secs) +
                      (e.fracsec - e0.fracsec) for e in b.epochs])
     epoch = e0 + float(np.sum(wt * offs))
-    out = DataBunch(**dict(b))
-    out.subints = sub.cpu().numpy()
-    out.weights = ws.cpu().numpy()
+    out = DataBunch(**{k: v for k, v in b.items()
+                       if k not in ("ok_isubs", "ok_ichans", "masks", "epoch_parts")})
+    out.weights = np.asarray(b.weights).sum(axis=0)[None]
     out.nsub = 1
     out.epochs = [epoch]
     out.subtimes = [float(dur.sum())]
@@ -114,7 +203,138 @@ def tscrunch(b, period_at=None):
     out.parallactic_angles = np.array([float(np.sum(wt * np.asarray(b.parallactic_angles)))])
     out.SNRs = np.sqrt(np.sum(np.asarray(b.SNRs) ** 2, axis=0))[None]
     out.noise_stds = None  # re-estimated from the averaged profiles (use_get_noise)
-    for k in ["ok_isubs", "ok_ichans", "masks"]:
+    return normalize(out, b.filename, subints=False)
+
+
+def dedispersion_phases(freqs, Ps, DM, nu_ref):
+    """Per-(subint, channel) rotation [rot] of arch.dedisperse() about nu_ref:
+    rotate_data(port, 0.0, DM, P, freqs, nu_ref) (pplib.py:2338-2426, the
+    reference's own convention: positive DM moves freqs < nu_ref earlier).
+    PSRCHIVE's dispersion constant is the reference's Dconst = 1/2.41e-4."""
+    f = np.asarray(freqs, dtype=np.float64)
+    return Dconst * DM * (f ** -2.0 - nu_ref ** -2.0) / np.asarray(Ps, dtype=np.float64)[:, None]
+
+
+class Archive:
+    """An opened archive: ``meta`` holds every load_data key but ``subints``
+    (after the requested processing); ``read(lo, hi)`` returns processed
+    subints [hi - lo, npol, nchan, nbin] -- a numpy array when nothing had to
+    run on the device, else a float64 device tensor."""
+
+    def __init__(self, filename, dedisperse=False, dededisperse=False, tscrunch=False,
+                 pscrunch=False, rm_baseline=True, quiet=True):
+        self.src = _source(filename, pscrunch)
+        raw = self.src.meta()
+        if not isinstance(filename, str):
+            filename = raw.get("filename", "archive")
+        raw.setdefault("filename", filename)
+        self.raw = raw
+        dmc = int(raw.get("dmc", 0))
+        self.rot_sign = 0.0
+        if dedisperse and not dmc:  # arch.dedisperse() (pplib.py:2686)
+            self.rot_sign, dmc = 1.0, 1
+        elif dededisperse and dmc:  # arch.dededisperse() (pplib.py:2687)
+            self.rot_sign, dmc = -1.0, 0
+        self.rm_base = bool(rm_baseline) and not raw.get("baseline_removed", True)
+        self.tscrunch = bool(tscrunch) and raw.nsub > 1
+        m = DataBunch(**dict(raw))
+        m.dmc = dmc
+        m.baseline_removed = bool(raw.get("baseline_removed", True) or rm_baseline)
+        if self.tscrunch:
+            m = _tscrunch_meta(m, getattr(self.src, "period_at", None))
+        self.meta = m
+        if not quiet:
+            print("\nReading data from %s on source %s..." % (filename, m.get("source", "")))
+
+    @property
+    def nsub(self):
+        return self.meta.nsub
+
+    def _process(self, sub, lo, hi):
+        """dedisperse / dededisperse, then remove_baseline, on subints lo:hi."""
+        if not self.rot_sign and not self.rm_base:
+            return sub
+        import torch
+        from .engine import get_engine
+        eng = get_engine()
+        r = self.raw
+        if _is_tensor(sub) and sub.device == eng.device:
+            d = sub.to(torch.float64).contiguous()
+            if d.data_ptr() == sub.data_ptr():
+                d = d.clone()  # never modify a caller's registered tensor
+        else:
+            d = torch.as_tensor(np.ascontiguousarray(sub, dtype=np.float64), device=eng.device)
+        n, npol, nchan, nbin = d.shape
+        if self.rot_sign:
+            ph = self.rot_sign * dedispersion_phases(r.freqs[lo:hi], r.Ps[lo:hi], r.DM, r.nu0)
+            eng.rotate_rows(d, np.repeat(ph[:, None, :], npol, axis=1), inplace=True)
+        if self.rm_base:
+            ntot = 2 if (npol >= 2 and str(r.get("state", "")).upper().startswith("COH")) else 1
+            eng.remove_baseline(d, r.weights[lo:hi], ntot=ntot, duty=DUTY_CYCLE)
+        return d
+
+    def read(self, lo=0, hi=None):
+        if self.tscrunch:  # the one averaged subint needs every raw subint
+            from .engine import get_engine
+            r = self.raw
+            sub = self._process(self.src.read(0, r.nsub), 0, r.nsub)
+            out, _ = get_engine().tscrunch(sub, r.weights)
+            return out
+        hi = self.meta.nsub if hi is None else hi
+        return self._process(self.src.read(lo, hi), lo, hi)
+
+
+def open_archive(filename, dedisperse=False, dededisperse=False, tscrunch=False, pscrunch=False,
+                 rm_baseline=True, quiet=True):
+    """Metadata now, subints on demand (see Archive)."""
+    return Archive(filename, dedisperse=dedisperse, dededisperse=dededisperse,
+                   tscrunch=tscrunch, pscrunch=pscrunch, rm_baseline=rm_baseline, quiet=quiet)
+
+
+def host_array(x):
+    """numpy view/copy of subints that may live on the device."""
+    if _is_tensor(x):
+        return x.detach().cpu().numpy()
+    return np.asarray(x)
+
+
+def load_data(filename, state=None, dedisperse=False, dededisperse=False, tscrunch=False,
+              pscrunch=False, fscrunch=False, rm_baseline=True, flux_prof=False,
+              refresh_arch=True, return_arch=True, quiet=False, get_SNRs=True, host=True):
+    """pplib.load_data (pplib.py:2650-2820) for a registered bunch, an .npz or
+    a fold-mode PSRFITS file.  host=False leaves device-resident subints on the
+    device.  noise_stds is get_noise_PS per profile (pplib.py:2740-2748), on the
+    device, unless the archive already holds it."""
+    if isinstance(filename, dict):
+        return normalize(filename)
+    if fscrunch:
+        raise NotImplementedError("load_data(fscrunch=True) is not on the fitting path")
+    a = open_archive(filename, dedisperse=dedisperse, dededisperse=dededisperse,
+                     tscrunch=tscrunch, pscrunch=pscrunch, rm_baseline=rm_baseline, quiet=quiet)
+    b = DataBunch(**dict(a.meta))
+    sub = a.read()
+    if b.get("noise_stds") is None and getattr(a.src, "eager_noise", False):
+        from .engine import get_engine
+        n, npol, nchan, nbin = tuple(sub.shape)
+        b.noise_stds = get_engine().noise_rows(sub.reshape(-1, nbin)).reshape(
+            n, npol, nchan).cpu().numpy()
+    b.subints = host_array(sub) if host else sub
+    for k in ("ok_isubs", "ok_ichans", "masks"):
+        b.pop(k, None)
+    return normalize(b, b.get("filename", filename))
+
+
+def tscrunch(b, period_at=None):
+    """load_data(tscrunch=True) of an already loaded bunch (ppf_tscrunch)."""
+    from .engine import get_engine
+    b = normalize(b, b.get("filename", "archive"))
+    if b.nsub == 1:
+        return b
+    m = _tscrunch_meta(b, period_at)
+    sub, _ = get_engine().tscrunch(b.subints, b.weights)
+    out = DataBunch(**dict(m))
+    out.subints = sub.cpu().numpy()
+    for k in ("ok_isubs", "ok_ichans", "masks"):
         out.pop(k, None)
     return normalize(out, b.filename)
 
@@ -128,7 +348,7 @@ SCALAR_KEYS = ["DM", "dmc", "backend", "frontend", "backend_delay", "telescope",
 def save_archive(path, bunch):
     """Write a normalised archive as .npz (numbers and strings only)."""
     b = normalize(bunch, os.path.basename(path))
-    arrs = {k: np.asarray(b[k]) for k in ARRAY_KEYS if b.get(k) is not None}
+    arrs = {k: host_array(b[k]) for k in ARRAY_KEYS if b.get(k) is not None}
     arrs["epochs"] = np.array([e.as_tuple() for e in b.epochs], dtype=np.float64)
     for k in SCALAR_KEYS:
         arrs["meta_" + k] = np.asarray(b[k])
@@ -143,37 +363,6 @@ def is_fits(filename):
             return f.read(9) == b"SIMPLE  ="
     except (OSError, TypeError):
         return False
-
-
-def load_data(filename, **kw):
-    """Archive by name: registered bunch, an .npz written by save_archive, or a
-    fold-mode PSRFITS file (psrfits.load_psrfits: host reader + device unpack)."""
-    if isinstance(filename, dict):
-        return normalize(filename)
-    if filename in _registry:
-        b = _registry[filename]
-        return tscrunch(b) if kw.get("tscrunch") else b
-    if isinstance(filename, str) and is_fits(filename):
-        from .psrfits import load_psrfits
-        return normalize(load_psrfits(filename, pscrunch=kw.get("pscrunch", False),
-                                      dededisperse=kw.get("dededisperse", False),
-                                      tscrunch=kw.get("tscrunch", False),
-                                      quiet=kw.get("quiet", True)), filename)
-    if isinstance(filename, str) and os.path.exists(filename) and filename.endswith(".npz"):
-        z = np.load(filename, allow_pickle=False)
-        b = {k: z[k] for k in z.files if not k.startswith("meta_") and k != "epochs"}
-        b["epochs"] = [MJD(int(d), int(s), f) for d, s, f in z["epochs"]]
-        for k in z.files:
-            if k.startswith("meta_"):
-                v = z[k]
-                b[k[5:]] = v.item() if v.ndim == 0 else v
-        for k in ["dmc"]:
-            if k in b:
-                b[k] = int(b[k])
-        b = normalize(b, filename)
-        return tscrunch(b) if kw.get("tscrunch") else b
-    raise RuntimeError("Cannot load_data(%s): not a registered, .npz or PSRFITS archive "
-                       "(other PSRCHIVE formats need PSRCHIVE)" % filename)
 
 
 def file_is_type(filename, filetype="ASCII"):

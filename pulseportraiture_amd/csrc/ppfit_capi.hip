@@ -1112,6 +1112,22 @@ int ppf_unpack_subints(ppf_ctx* ctx, int32_t nsub, int32_t npol, int32_t nchan, 
   });
 }
 
+int ppf_remove_baseline(ppf_ctx* ctx, int32_t nsub, int32_t npol, int32_t nchan, int32_t nbin,
+                        int32_t ntot, int32_t width, double* data, const double* weights,
+                        int32_t* window) {
+  if (!ctx || !data || !weights) return fail(ctx, PPF_ERR_INVALID, "null argument");
+  if (nsub <= 0) return PPF_OK;
+  if (npol <= 0 || nchan <= 0 || nbin <= 0 || nbin > 8192)
+    return fail(ctx, PPF_ERR_INVALID, "bad shape (%d, %d, %d)", npol, nchan, nbin);
+  if (ntot < 1 || ntot > npol) return fail(ctx, PPF_ERR_INVALID, "ntot %d with npol %d", ntot, npol);
+  if (width < 1 || width > nbin) return fail(ctx, PPF_ERR_INVALID, "width %d", width);
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  return timed(ctx, PPF_K_UNPACK, [&] {
+    hipLaunchKernelGGL(k_remove_baseline, dim3(nsub), dim3(256), (size_t)nbin * sizeof(double),
+                       ctx->stream, data, weights, npol, nchan, nbin, ntot, width, window);
+  });
+}
+
 int ppf_resid_chi2_rows(ppf_ctx* ctx, int32_t nrow, int32_t nbin, const double* data,
                         const double* phase, const double* model, const int32_t* model_row,
                         const double* scale, const double* tau, const double* errs,

@@ -321,6 +321,85 @@ __global__ void k_unpack(const T* __restrict__ raw, const double* __restrict__ s
   out[i] = v;
 }
 
+// ---------------------------------------------------------------------------
+// remove_baseline (load_data's arch.remove_baseline(), pplib.py:2691), as
+// PSRCHIVE's Integration::remove_baseline does it with the default baseline
+// estimator: the off-pulse window is found once per subint on the total
+// intensity profile (weighted frequency sum of the first ntot polarisations)
+// as the circular window of `width` bins with the smallest sum (the minimum of
+// the boxcar-smoothed profile; first window on ties), and every profile of
+// the subint has its own mean over that window subtracted.  One workgroup per
+// subint: t[j] in LDS (coalesced channel rows), each thread sums the windows
+// that start at its bins directly (no prefix-sum cancellation), a block argmin,
+// then one wave per profile row: window mean (wave sum), row -= mean in place.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_remove_baseline(double* __restrict__ data,
+                                                         const double* __restrict__ w, int npol,
+                                                         int nchan, int nbin, int ntot, int width,
+                                                         int* __restrict__ win_out) {
+  extern __shared__ __align__(16) unsigned char dyn[];
+  double* t = reinterpret_cast<double*>(dyn);  // [nbin]
+  __shared__ double bv[4];
+  __shared__ int bi[4];
+  __shared__ int s_j0;
+  const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  double* sub = data + (size_t)s * npol * nchan * nbin;
+  const double* ws = w + (size_t)s * nchan;
+  for (int j = tid; j < nbin; j += 256) {
+    double acc = 0.0;
+    for (int n = 0; n < nchan; ++n) {
+      const double wn = ws[n];
+      if (wn == 0.0) continue;  // uniform over the block
+      double v = 0.0;
+      for (int p = 0; p < ntot; ++p) v += sub[((size_t)p * nchan + n) * nbin + j];
+      acc = fma(wn, v, acc);
+    }
+    t[j] = acc;
+  }
+  __syncthreads();
+  double best = INFINITY;
+  int bj = 0x7fffffff;
+  for (int j = tid; j < nbin; j += 256) {
+    double b = 0.0;
+    for (int i = 0; i < width; ++i) {
+      int k = j + i;
+      if (k >= nbin) k -= nbin;
+      b += t[k];
+    }
+    if (b < best || (b == best && j < bj)) { best = b; bj = j; }
+  }
+  // block argmin, first index on ties
+  for (int o = 32; o >= 1; o >>= 1) {
+    const double ob = __shfl_xor(best, o);
+    const int oj = __shfl_xor(bj, o);
+    if (ob < best || (ob == best && oj < bj)) { best = ob; bj = oj; }
+  }
+  if (lane == 0) { bv[wv] = best; bi[wv] = bj; }
+  __syncthreads();
+  if (tid == 0) {
+    double b = bv[0];
+    int j0 = bi[0];
+    for (int q = 1; q < 4; ++q)
+      if (bv[q] < b || (bv[q] == b && bi[q] < j0)) { b = bv[q]; j0 = bi[q]; }
+    s_j0 = j0;
+    if (win_out) win_out[s] = j0;
+  }
+  __syncthreads();
+  const int j0 = s_j0;
+  const double iw = 1.0 / (double)width;
+  for (int r = wv; r < npol * nchan; r += 4) {
+    double* row = sub + (size_t)r * nbin;
+    double m = 0.0;
+    for (int i = lane; i < width; i += 64) {
+      int k = j0 + i;
+      if (k >= nbin) k -= nbin;
+      m += row[k];
+    }
+    m = wave_sum(m) * iw;
+    for (int j = lane; j < nbin; j += 64) row[j] -= m;
+  }
+}
+
 template __global__ void k_unpack<uint8_t>(const uint8_t*, const double*, const double*, int, int,
                                            int, int, int, double*);
 template __global__ void k_unpack<int16_t>(const int16_t*, const double*, const double*, int, int,

@@ -333,13 +333,18 @@ class Engine:
         out._keep = (d, m, nz, mi)
         return out
 
-    def rotate_rows(self, rows, phase):
+    def rotate_rows(self, rows, phase, inplace=False):
+        """irfft(rfft(row) e^{2 pi i k phase}) per row; inplace=True writes
+        back into a contiguous float64 device tensor (each row is read whole
+        into LDS before it is written)."""
         dev = self.device
         r = _dev_f64(rows, dev)
         shape = r.shape
         r = r.reshape(-1, shape[-1])
         ph = _dev_f64(phase, dev).reshape(-1).expand(r.shape[0]).contiguous()
-        out = torch.empty_like(r)
+        if inplace and not (isinstance(rows, torch.Tensor) and rows.data_ptr() == r.data_ptr()):
+            raise PPFitError("rotate_rows(inplace=True) needs a contiguous float64 device tensor")
+        out = r if inplace else torch.empty_like(r)
         self._chk(self.lib.ppf_rotate_rows(self.ctx, r.shape[0], r.shape[1], _ptr(r),
                                            _ptr(ph), _ptr(out)))
         out._keep = (r, ph)
@@ -455,6 +460,24 @@ class Engine:
                                         _ptr(out), _ptr(ws)))
         out._keep = (d, w)
         return out, ws
+
+    def remove_baseline(self, subints, weights, ntot=1, duty=0.15):
+        """arch.remove_baseline() in place (ppf_remove_baseline): subints is a
+        float64 device tensor [nsub, npol, nchan, nbin], weights [nsub, nchan].
+        Returns the per-subint baseline window starts (int32 device tensor)."""
+        d = subints
+        if not (isinstance(d, torch.Tensor) and d.device == self.device and
+                d.dtype == torch.float64 and d.is_contiguous() and d.dim() == 4):
+            raise PPFitError("remove_baseline: need a contiguous float64 [nsub, npol, nchan, "
+                             "nbin] tensor on %s" % self.device)
+        nsub, npol, nchan, nbin = d.shape
+        w = _dev_f64(weights, self.device).reshape(nsub, nchan).contiguous()
+        width = max(1, int(duty * nbin))
+        win = torch.empty(nsub, dtype=torch.int32, device=self.device)
+        self._chk(self.lib.ppf_remove_baseline(self.ctx, nsub, npol, nchan, nbin, int(ntot), width,
+                                               _ptr(d), _ptr(w), _ptr(win)))
+        win._keep = w
+        return win
 
     def irfft_rows(self, spec, nbin):
         dev = self.device

@@ -48,42 +48,138 @@ def allreduce_sum(*tensors):
     return tensors
 
 
-def _units(datafiles, model_data, SNR_cutoff, quiet, skip_these, state=None, tscrunch=False):
-    """Load archives and list (archive, subint, ichans, model_ichans) units."""
-    units, archives = [], {}
+def _open_all(datafiles, model_data, SNR_cutoff, quiet, skip_these, tscrunch, pscrunch):
+    """Metadata of every archive (ppalign.py:121-159's checks, no DATA read):
+    [(name, Archive)] of the archives to align."""
+    out = []
     for name in datafiles:
-        try:
-            data = _arch.load_data(name, tscrunch=tscrunch)  # ppalign.py:123-127
+        try:  # ppalign.py:123-127 (rm_baseline False: F0_fact = 0, pptoas.py:26-29)
+            a = _arch.open_archive(name, dedisperse=False, tscrunch=tscrunch, pscrunch=pscrunch,
+                                   rm_baseline=rm_baseline, quiet=True)
         except RuntimeError:
             if not quiet:
                 print("%s: cannot load_data().  Skipping it." % name)
             skip_these.append(name)
             continue
-        if data.nbin != model_data.nbin:
+        m = a.meta
+        if m.nbin != model_data.nbin:
             if not quiet:
-                print("%s: %d != %d phase bins.  Skipping it." % (name, data.nbin,
-                                                                 model_data.nbin))
+                print("%s: %d != %d phase bins.  Skipping it." % (name, m.nbin, model_data.nbin))
             skip_these.append(name)
             continue
-        if data.prof_SNR < SNR_cutoff:
+        if m.prof_SNR < SNR_cutoff:
+            if not quiet:
+                print("%s: %d < %d S/N cutoff.  Skipping it." % (name, m.prof_SNR, SNR_cutoff))
             skip_these.append(name)
             continue
+        out.append((name, a))
+    return out
+
+
+def _units(opened, model_data):
+    """(name, subint, ichans, model_ichans) per ok subint (ppalign.py:153-177)."""
+    units = []
+    mf = model_data.freqs[0]
+    for name, a in opened:
+        m = a.meta
         try:
-            fd = data.freqs - model_data.freqs
+            fd = m.freqs - model_data.freqs
             same = fd.min() == fd.max() == 0.0
         except ValueError:
             same = False
-        archives[name] = data
-        for isub in data.ok_isubs:
+        for isub in m.ok_isubs:
             if same:
-                ichans = np.intersect1d(data.ok_ichans[isub], model_data.ok_ichans[0])
+                ichans = np.intersect1d(m.ok_ichans[isub], model_data.ok_ichans[0])
                 mich = ichans
             else:
-                ichans = np.asarray(data.ok_ichans[isub])
-                mich = np.array([np.argmin(abs(model_data.freqs[0] - data.freqs[isub, c]))
-                                 for c in ichans])
+                ichans = np.asarray(m.ok_ichans[isub])
+                mich = np.array([np.argmin(abs(mf - m.freqs[isub, c])) for c in ichans])
             units.append((name, int(isub), ichans, mich))
-    return units, archives
+    return units
+
+
+class _UnitStack:
+    """Device-resident inputs of this rank's units, built once and reused by
+    every iteration (the reference re-reads every archive per iteration,
+    ppalign.py:121-127; the data do not change): unit channel c sits in
+    template slot mich[c], other slots are masked."""
+
+    def __init__(self, eng, units, opened, model_freqs, npol, nchan, nbin):
+        dev = eng.device
+        n = len(units)
+        f64 = dict(dtype=torch.float64, device=dev)
+        self.n = n
+        self.pols = [torch.zeros((n, nchan, nbin), **f64) for _ in range(npol)]
+        freqs = np.tile(np.asarray(model_freqs, dtype=np.float64), (n, 1))
+        errs = np.ones((n, nchan))
+        mask = np.zeros((n, nchan), dtype=np.uint8)
+        wts = np.zeros((n, nchan))
+        P, DMg, nu_fit = np.zeros(n), np.zeros(n), np.zeros(n)
+        need_noise = np.zeros(n, dtype=bool)
+        arch = dict(opened)
+        by_arch = {}
+        for i, u in enumerate(units):
+            by_arch.setdefault(u[0], []).append(i)
+        for name, idx in by_arch.items():
+            a = arch[name]
+            m = a.meta
+            isubs = [units[i][1] for i in idx]
+            lo, hi = min(isubs), max(isubs) + 1
+            sub = a.read(lo, hi)  # this rank's subint range only
+            if not isinstance(sub, torch.Tensor):
+                sub = torch.as_tensor(np.ascontiguousarray(sub), device=dev)
+            ns = m.get("noise_stds")
+            for i in idx:
+                _, isub, ichans, mich = units[i]
+                full = len(ichans) == nchan and np.array_equal(mich, np.arange(nchan)) and \
+                    np.array_equal(ichans, mich)
+                if full:
+                    for ipol in range(npol):
+                        self.pols[ipol][i].copy_(sub[isub - lo, ipol])
+                else:
+                    ic = torch.as_tensor(ichans, device=dev, dtype=torch.long)
+                    mc = torch.as_tensor(mich, device=dev, dtype=torch.long)
+                    for ipol in range(npol):
+                        self.pols[ipol][i].index_copy_(0, mc,
+                                                       sub[isub - lo, ipol].index_select(0, ic))
+                freqs[i, mich] = m.freqs[isub, ichans]
+                if ns is not None:
+                    errs[i, mich] = np.asarray(ns)[isub, 0, ichans]
+                else:
+                    need_noise[i] = True
+                mask[i, mich] = 1
+                wts[i, mich] = m.weights[isub, ichans]
+                P[i] = m.Ps[isub]
+                DMg[i] = m.DM
+                nu_fit[i] = guess_fit_freq(m.freqs[isub, ichans], m.SNRs[isub, 0, ichans])
+        if need_noise.any():  # load_data's noise_stds (pplib.py:2744-2748), on the device
+            noise = eng.noise_rows(self.pols[0].reshape(-1, nbin)).reshape(n, nchan).cpu().numpy()
+            errs = np.where(need_noise[:, None] & (mask > 0), noise, errs)
+        self.freqs, self.errs, self.mask, self.wts = freqs, errs, mask, wts
+        self.P, self.DMg, self.nu_fit = P, DMg, nu_fit
+
+    def fit_and_accumulate(self, eng, model_port, fit_dm, accum, tw):
+        """One iteration's fits (ppalign.py:178-195) and weighted rotate-and-sum
+        (ppalign.py:202-208) in the Fourier domain."""
+        n = self.n
+        init = np.stack([np.zeros(n), self.DMg, np.zeros(n), np.zeros(n), np.zeros(n)], 1)
+        flags = [1, int(bool(fit_dm)), 0, 0, 0]
+        res = fit_portraits_batch(self.pols[0], model_port, init, self.P, self.freqs,
+                                  nu_fits=np.stack([self.nu_fit] * 3, 1), errs=self.errs,
+                                  fit_flags=flags, log10_tau=False, chan_mask=self.mask,
+                                  weights=self.wts, guess=True, guess_Ns=model_port.shape[1],
+                                  guess_wrap=False, guess_nu=self.nu_fit)
+        phase = res["params"][:, 0]
+        DM = res["params"][:, 1]
+        nu_ref = res["nu_out"][:, 0]
+        # rotate_data(port, phase, DM, P, freqs, nu_ref) per channel (pplib.py:2406-2415)
+        ph = phase[:, None] + (Dconst * DM / self.P)[:, None] * \
+            (self.freqs ** -2.0 - nu_ref[:, None] ** -2.0)
+        w = np.where(self.mask > 0, res["scales"] / self.errs ** 2, 0.0)
+        for ipol, pol in enumerate(self.pols):
+            eng.rotate_accumulate(pol, ph, w, accum[ipol])
+        tw += torch.as_tensor(w.sum(axis=0), device=tw.device)
+        return res
 
 
 def align_archives(metafile, initial_guess, fit_dm=True, tscrunch=False, pscrunch=True,
@@ -102,7 +198,9 @@ def align_archives(metafile, initial_guess, fit_dm=True, tscrunch=False, pscrunc
             outfile = metafile + ".algnd.fits"
     else:
         datafiles = list(metafile) if not isinstance(metafile, str) else [metafile]
-    model_data = _arch.load_data(initial_guess, tscrunch=True)  # ppalign.py:103-106
+    # the initial guess: dedispersed, tscrunched, baseline removed (ppalign.py:103-106)
+    model_data = _arch.load_data(initial_guess, dedisperse=True, dededisperse=False,
+                                 tscrunch=True, pscrunch=pscrunch, rm_baseline=True, quiet=quiet)
     npol = 1 if pscrunch else model_data.npol
     model_port = np.asarray((model_data.masks * model_data.subints)[0, 0], dtype=np.float64)
     nchan, nbin = model_port.shape
@@ -111,10 +209,20 @@ def align_archives(metafile, initial_guess, fit_dm=True, tscrunch=False, pscrunc
     dev = eng.device
     rank, world = dist_info()
     skip_these = []
-    units, archives = _units(datafiles, model_data, SNR_cutoff, quiet, skip_these,
-                             tscrunch=tscrunch)
+    opened = _open_all(datafiles, model_data, SNR_cutoff, quiet, skip_these, tscrunch, pscrunch)
+    units = _units(opened, model_data)
     lo, hi = shard_range(len(units), rank, world)
     mine = units[lo:hi]
+    multi = [u for u in mine if len(u[2]) > 1]
+    single = [u for u in mine if len(u[2]) <= 1]
+    stack = _UnitStack(eng, multi, opened, model_data.freqs[0], npol, nchan, nbin) \
+        if multi else None
+    archives = {}
+    for name, a in opened:  # 1-channel hack units (rare): their archives on the host
+        if any(u[0] == name for u in single):
+            archives[name] = _arch.load_data(name, dedisperse=False, tscrunch=tscrunch,
+                                             pscrunch=pscrunch, rm_baseline=rm_baseline,
+                                             quiet=True)
     count = 1
     aligned = None
     tw = None
@@ -123,11 +231,8 @@ def align_archives(metafile, initial_guess, fit_dm=True, tscrunch=False, pscrunc
             print("Doing iteration %d..." % count)
         accum = torch.zeros(npol, nchan, nharm, 2, dtype=torch.float64, device=dev)
         tw = torch.zeros(nchan, dtype=torch.float64, device=dev)
-        multi = [u for u in mine if len(u[2]) > 1]
-        single = [u for u in mine if len(u[2]) <= 1]
-        if multi:
-            _fit_and_accumulate(eng, multi, archives, model_port, model_data.freqs[0],
-                                fit_dm, npol, accum, tw)
+        if stack is not None:
+            stack.fit_and_accumulate(eng, model_port, fit_dm, accum, tw)
         for u in single:  # 1-channel hack, ppalign.py:196-201
             _single_channel(u, archives, model_port, npol, accum, tw, dev)
         allreduce_sum(accum, tw)
@@ -157,53 +262,6 @@ def align_archives(metafile, initial_guess, fit_dm=True, tscrunch=False, pscrunc
     if return_weights:
         return aligned, tw.cpu().numpy()
     return aligned
-
-
-def _fit_and_accumulate(eng, units, archives, model_port, model_freqs, fit_dm, npol,
-                        accum, tw):
-    nchan, nbin = model_port.shape
-    n = len(units)
-    data = np.zeros((n, nchan, nbin))
-    freqs = np.zeros((n, nchan))
-    errs = np.ones((n, nchan))
-    mask = np.zeros((n, nchan), dtype=np.uint8)
-    wts = np.zeros((n, nchan))
-    P = np.zeros(n)
-    DMg = np.zeros(n)
-    nu_fit = np.zeros(n)
-    for i, (name, isub, ichans, mich) in enumerate(units):
-        d = archives[name]
-        # unit channel c sits in template slot mich[c]; other slots are masked
-        data[i, mich] = d.subints[isub, 0, ichans]
-        freqs[i] = model_freqs
-        freqs[i, mich] = d.freqs[isub, ichans]
-        noise = d.noise_stds[isub, 0, ichans] if d.get("noise_stds") is not None else \
-            eng.noise_rows(d.subints[isub, 0, ichans]).cpu().numpy()
-        errs[i, mich] = noise
-        mask[i, mich] = 1
-        wts[i, mich] = d.weights[isub, ichans]
-        P[i] = d.Ps[isub]
-        DMg[i] = d.DM
-        nu_fit[i] = guess_fit_freq(d.freqs[isub, ichans], d.SNRs[isub, 0, ichans])
-    init = np.stack([np.zeros(n), DMg, np.zeros(n), np.zeros(n), np.zeros(n)], 1)
-    flags = [1, int(bool(fit_dm)), 0, 0, 0]
-    res = fit_portraits_batch(data, model_port, init, P, freqs,
-                              nu_fits=np.stack([nu_fit] * 3, 1), errs=errs, fit_flags=flags,
-                              log10_tau=False, chan_mask=mask, weights=wts, guess=True,
-                              guess_Ns=nbin, guess_wrap=False, guess_nu=nu_fit)
-    phase = res["params"][:, 0]
-    DM = res["params"][:, 1]
-    nu_ref = res["nu_out"][:, 0]
-    # rotate_data(port, phase, DM, P, freqs, nu_ref) per channel (pplib.py:2406-2415)
-    ph = phase[:, None] + (Dconst * DM / P)[:, None] * (freqs ** -2.0 - nu_ref[:, None] ** -2.0)
-    w = np.where(mask > 0, res["scales"] / errs ** 2, 0.0)
-    for ipol in range(npol):
-        pol = np.zeros((n, nchan, nbin))
-        for i, (name, isub, ichans, mich) in enumerate(units):
-            pol[i, mich] = archives[name].subints[isub, ipol, ichans]
-        eng.rotate_accumulate(pol, ph, w, accum[ipol])
-    tw += torch.as_tensor(w.sum(axis=0), device=tw.device)
-    return res
 
 
 def _single_channel(u, archives, model_port, npol, accum, tw, dev):

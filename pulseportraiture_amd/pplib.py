@@ -501,34 +501,51 @@ def filter_TOAs(TOAs, flag, cutoff, criterion=">=", pass_unflagged=False,
     return keep
 
 
-def _flag_text(flag, value):
-    """Python-2 formatting of write_TOAs (pplib.py:3486-3503): str %s, int %d."""
-    if hasattr(value, "lower"):
-        return " -%s %s" % (flag, value)
-    if isinstance(value, (int, np.integer)) and not isinstance(value, bool):
-        return " -%s %d" % (flag, value)
+def _flag_fmt(flag, vtype):
+    """Format of one flag in write_TOAs' Python-2 formatting (pplib.py:3486-3503)
+    for a value of type vtype: str %s, int %d, '_cov' %.1e, 'phs' %.8f, 'flux'
+    %.5f, else %.3f."""
+    f = flag.replace("%", "%%")
+    if hasattr(vtype, "lower"):
+        return " -%s %%s" % f
+    if issubclass(vtype, (int, np.integer)) and not issubclass(vtype, (bool, np.bool_)):
+        return " -%s %%d" % f
     if flag.find("_cov") >= 0:
-        return " -%s %.1e" % (flag, value)
+        return " -%s %%.1e" % f
     if flag.find("phs") >= 0:
-        return " -%s %.8f" % (flag, value)
+        return " -%s %%.8f" % f
     if flag.find("flux") >= 0:
-        return " -%s %.5f" % (flag, value)
-    return " -%s %.3f" % (flag, value)
+        return " -%s %%.5f" % f
+    return " -%s %%.3f" % f
+
+
+def _flag_text(flag, value):
+    """One flag as write_TOAs prints it (pplib.py:3486-3503)."""
+    return _flag_fmt(flag, type(value)) % value
+
+
+_LINE_FMTS = {}  # (flag, type) signature of a TOA's flags -> their joined format
 
 
 def toa_line(toa, inf_is_zero=True):
-    """One loosely-IPTA .tim line, pplib.py:3471-3503."""
+    """One loosely-IPTA .tim line, pplib.py:3471-3503.  The flags of every TOA
+    with the same (flag, value type) signature share one format string."""
     freq = 0.0 if (toa.frequency == np.inf and inf_is_zero) else toa.frequency
-    s = "%s %.8f %d" % (toa.archive, freq, toa.MJD.intday()) + \
-        ("%.15f   %.3f  %s" % (toa.MJD.fracday(), toa.TOA_error, toa.telescope_code))[1:]
+    m = toa.MJD
+    s = "%s %.8f %d" % (toa.archive, freq, m.intday()) + \
+        ("%.15f   %.3f  %s" % (m.fracday(), toa.TOA_error, toa.telescope_code))[1:]
     if toa.DM is not None:
         s += " -pp_dm %.7f" % toa.DM
     if toa.DM_error is not None:
         s += " -pp_dme %.7f" % toa.DM_error
-    for flag, value in toa.flags.items():
-        if value is not None:
-            s += _flag_text(flag, value)
-    return s
+    items = [(k, v) for k, v in toa.flags.items() if v is not None]
+    sig = tuple([(k, type(v)) for k, v in items])
+    fmt = _LINE_FMTS.get(sig)
+    if fmt is None:
+        fmt = "".join([_flag_fmt(k, t) for k, t in sig])
+        if len(_LINE_FMTS) < 4096:
+            _LINE_FMTS[sig] = fmt
+    return s + fmt % tuple([v for _, v in items])
 
 
 def write_TOAs(TOAs, inf_is_zero=True, SNR_cutoff=0.0, outfile=None, append=True):

@@ -7,12 +7,13 @@ and assembles TOA records, Doppler-corrected DMs, flags and the DeltaDM mean
 on the host.  Archives come from ``archive.load_data`` (PSRCHIVE is out of
 scope; see archive.py).
 """
+import gc
 import time
 
 import numpy as np
 
 from . import archive as _arch
-from .mjd import MJD
+from .mjd import MJD, add_days, epoch_parts
 from .pplib import (DataBunch, F0_fact, phase_transform, guess_fit_freq, read_model,
                     load_spline_model_file,
                     read_model_device, gen_gaussian_portraits_device, scattering_alpha,
@@ -42,7 +43,12 @@ def _shard_range(n, rank, world):
 
 
 class TOA:
-    """TOA record, pptoas.py:31-73."""
+    """TOA record, pptoas.py:31-73.  The reference sets every flag as an
+    attribute (pptoas.py:70-72); here the base fields are slots and a flag
+    attribute reads through to ``flags`` (attributes set later live in the
+    instance dict, which shadows a flag of the same name)."""
+    __slots__ = ("archive", "frequency", "MJD", "TOA_error", "telescope", "telescope_code",
+                 "DM", "DM_error", "flags", "__dict__")
 
     def __init__(self, archive, frequency, MJD, TOA_error, telescope, telescope_code,
                  DM=None, DM_error=None, flags={}):
@@ -55,8 +61,14 @@ class TOA:
         self.DM = DM
         self.DM_error = DM_error
         self.flags = flags
-        for k, v in flags.items():
-            setattr(self, k, v)
+
+    def __getattr__(self, name):  # only when no slot / instance attribute has it
+        if name != "flags":
+            try:
+                return self.flags[name]
+            except (KeyError, AttributeError):
+                pass
+        raise AttributeError("'TOA' object has no attribute %r" % name)
 
     def write_TOA(self, inf_is_zero=True, outfile=None):
         return write_TOAs(self, inf_is_zero=inf_is_zero, outfile=outfile, append=True)
@@ -90,14 +102,39 @@ class GetTOAs:
         self.instrumental_response_dict = self.ird = {"DM": 0.0, "wids": [], "irf_types": []}
         self.quiet = quiet
 
+    def _fits_model(self, nchan_data=None):
+        """The FITS-archive template of get_TOAs (pptoas.py:323-338): tscrunched,
+        baseline removed, masked; [nchan, nbin] (a 1-channel template tiled)."""
+        md = _arch.load_data(self.modelfile, dedisperse=False, dededisperse=False,
+                             tscrunch=True, pscrunch=True, rm_baseline=True, quiet=True)
+        model = np.asarray((md.masks * md.subints)[0, 0])
+        if md.nchan == 1 and nchan_data is not None:
+            model = np.tile(model[0], nchan_data).reshape(nchan_data, md.nbin)
+        return md, model
+
+    @staticmethod
+    def _row_keys(rows):
+        """First-appearance index of every distinct row, and each row's index
+        into those (np.unique on the rows, renumbered in order of appearance)."""
+        rows = np.ascontiguousarray(rows)
+        if (rows == rows[0]).all():
+            return np.zeros(1, dtype=np.int64), np.zeros(len(rows), dtype=np.int64)
+        v = rows.view(np.dtype((np.void, rows.dtype.itemsize * rows.shape[1]))).ravel()
+        _, first, inv = np.unique(v, return_index=True, return_inverse=True)
+        order = np.argsort(first, kind="stable")
+        rank = np.empty_like(order)
+        rank[order] = np.arange(len(order))
+        return first[order], rank[inv.ravel()]
+
     # -- per-subint templates ------------------------------------------------
     def _models(self, data, fit_scat, quiet):
-        """Template portrait per ok subint (pptoas.py:351-378), de-duplicated."""
+        """Template portrait per ok subint (pptoas.py:351-378), de-duplicated:
+        one device build per distinct (channel frequencies, P when TAU is in
+        bins of P) key."""
         nsub = data.nsub
         if self.is_FITS_model:
-            md = _arch.load_data(self.modelfile)
-            model = (md.masks * md.subints)[0, 0]
-            if md.nbin != data.nbin or md.nchan != data.nchan:
+            md, model = self._fits_model(data.nchan)
+            if md.nbin != data.nbin or md.nchan != data.nchan:  # pptoas.py:329-338
                 return None
             return np.asarray(model)[None], np.zeros(nsub, dtype=np.int32), None
         try:
@@ -109,37 +146,30 @@ class GetTOAs:
         if fit_scat:
             self.model_code, self.model_nu_ref = code, nu_ref
             self.gparams, self.alpha = gparams, alpha
-        # one template per distinct (freqs, P-if-scattered) key, all built on
-        # the device (ppf_gaussian_portraits): read_model per subint in the
-        # reference (pptoas.py:351-378); fit_scat builds the unscattered one
-        cache, keyf, keyP, idx = {}, [], [], np.zeros(nsub, dtype=np.int32)
         tau_P = gparams[1] != 0 and not fit_scat
-        for isub in data.ok_isubs:
-            P = data.Ps[isub]
-            f = data.freqs[isub]
-            key = (f.tobytes(), P if tau_P else None)
-            if key not in cache:
-                cache[key] = len(keyf)
-                keyf.append(f)
-                keyP.append(P)
-            idx[isub] = cache[key]
+        ok = np.asarray(data.ok_isubs)
+        keyrows = data.freqs[ok]
+        if tau_P:
+            keyrows = np.concatenate([keyrows, data.Ps[ok][:, None]], axis=1)
+        first, inv = self._row_keys(keyrows)
+        idx = np.zeros(nsub, dtype=np.int32)
+        idx[ok] = inv
+        keyf = data.freqs[ok[first]]
+        keyP = data.Ps[ok[first]]
         nbin = len(data.phases)
-        models = np.empty((len(keyf), data.nchan, nbin))
+        models = np.empty((len(first), data.nchan, nbin))
         params = np.array(gparams, dtype=float)
         if fit_scat:
             params[1] = 0.0
-            models[:] = gen_gaussian_portraits_device(code, params, 0.0, nbin, np.array(keyf),
-                                                      nu_ref)
+            models[:] = gen_gaussian_portraits_device(code, params, 0.0, nbin, keyf, nu_ref)
         elif not tau_P:
-            models[:] = gen_gaussian_portraits_device(code, params, alpha, nbin, np.array(keyf),
-                                                      nu_ref)
+            models[:] = gen_gaussian_portraits_device(code, params, alpha, nbin, keyf, nu_ref)
         else:  # read_model's TAU * nbin / P differs per period
-            for P in sorted(set(keyP)):
-                sel = [i for i, q in enumerate(keyP) if q == P]
+            for P in sorted(set(keyP.tolist())):
+                sel = np.flatnonzero(keyP == P)
                 pp = np.copy(params)
                 pp[1] *= nbin / P
-                models[sel] = gen_gaussian_portraits_device(code, pp, alpha, nbin,
-                                                            np.array([keyf[i] for i in sel]),
+                models[sel] = gen_gaussian_portraits_device(code, pp, alpha, nbin, keyf[sel],
                                                             nu_ref)
         return models, idx, None
 
@@ -149,14 +179,12 @@ class GetTOAs:
         frequency row (ppf_spline_portraits)."""
         name, source, datafile, mean_prof, eigvec, tck = load_spline_model_file(self.modelfile)
         self.model_name = name
-        cache, keyf, idx = {}, [], np.zeros(data.nsub, dtype=np.int32)
-        for isub in data.ok_isubs:
-            f = data.freqs[isub]
-            idx[isub] = cache.setdefault(f.tobytes(), len(keyf))
-            if idx[isub] == len(keyf):
-                keyf.append(f)
+        ok = np.asarray(data.ok_isubs)
+        first, inv = self._row_keys(data.freqs[ok])
+        idx = np.zeros(data.nsub, dtype=np.int32)
+        idx[ok] = inv
         from .engine import get_engine
-        models = get_engine().spline_portraits(mean_prof, eigvec, tck, np.array(keyf),
+        models = get_engine().spline_portraits(mean_prof, eigvec, tck, data.freqs[ok[first]],
                                                len(data.phases)).cpu().numpy()
         return models, idx, None
 
@@ -189,15 +217,45 @@ class GetTOAs:
             idx[isub] = keys[key]
         return np.stack(out), idx
 
+    def _open(self, datafile, tscrunch, quiet, rm_base=None):
+        """open_archive as get_TOAs loads (pptoas.py:250-264): no
+        dedispersion; a dedispersed archive (dmc = 1) is reopened with
+        dededisperse=True."""
+        rb = rm_baseline if rm_base is None else rm_base
+        a = _arch.open_archive(datafile, dedisperse=False, dededisperse=False, tscrunch=tscrunch,
+                               pscrunch=True, rm_baseline=rb, quiet=quiet)
+        if a.meta.dmc:
+            if not quiet:
+                print("%s is dedispersed (dmc = 1).  Reloading it." % datafile)
+            a = _arch.open_archive(datafile, dedisperse=False, dededisperse=True,
+                                   tscrunch=tscrunch, pscrunch=True, rm_baseline=rb,
+                                   quiet=quiet)
+        return a
+
+    def _load(self, datafile, tscrunch, quiet, rm_base):
+        """load_data as the reference's drivers call it (pptoas.py:808-820,
+        1329-1344): reloaded with dededisperse=True when dmc = 1."""
+        a = self._open(datafile, tscrunch, quiet, rm_base)
+        b = DataBunch(**dict(a.meta))
+        b.subints = _arch.host_array(a.read())
+        return b
+
     def get_TOAs(self, datafile=None, tscrunch=False, nu_refs=None, DM0=None, bary=True,
                  fit_DM=True, fit_GM=False, fit_scat=False, log10_tau=True, scat_guess=None,
                  fix_alpha=False, print_phase=False, print_flux=False, print_parangle=False,
                  add_instrumental_response=False, addtnl_toa_flags={}, method="trust-ncg",
                  bounds=None, nu_fits=None, show_plot=False, quiet=None):
-        """pptoas.py:150-738 with the subint loop batched on the device."""
+        """pptoas.py:150-738 with the subint loop batched on the device.
+
+        Every archive is opened for its metadata first (no DATA read); the
+        (archive, subint) units in get_TOAs order are split into contiguous
+        shards, one per rank of an initialised torch.distributed group, and a
+        rank reads only the subint range of its shard (pptoas.py:246,343 is the
+        loop being sharded).  Fits run in one device call per archive and flag
+        set; the per-subint result rows are all-gathered, and every rank
+        assembles the same TOAs in the reference's order."""
         if quiet is None:
             quiet = self.quiet
-        already_warned = False
         warning = "You are using an experimental functionality of pptoas!"
         self.nfit = 1 + int(fit_DM) + int(fit_GM) + 2 * int(fit_scat) - int(fix_alpha)
         self.fit_phi, self.fit_DM, self.fit_GM = True, fit_DM, fit_GM
@@ -209,10 +267,8 @@ class GetTOAs:
         self.log10_tau = log10_tau
         if not fit_scat:
             self.log10_tau = log10_tau = False
-        if self.fit_GM or fit_scat:
-            if not quiet:
-                print(warning)
-            already_warned = True
+        if (self.fit_GM or fit_scat) and not quiet:
+            print(warning)
         self.scat_guess = scat_guess
         self.DM0, self.bary = DM0, bary
         self.tscrunch = tscrunch
@@ -220,16 +276,13 @@ class GetTOAs:
         self._fit_flags_prev = None  # the reference's loop-carried fit_flags
         start = time.time()
         datafiles = self.datafiles if datafile is None else [datafile]
-        # 1. load and prepare every archive (all ranks: host bookkeeping only)
+        # 1. metadata of every archive (all ranks; no DATA read)
         jobs = []
         for iarch, datafile in enumerate(datafiles):
             try:
-                data = _arch.load_data(datafile, dedisperse=False, dededisperse=False,
-                                       tscrunch=tscrunch, pscrunch=True, rm_baseline=rm_baseline,
-                                       quiet=quiet)
-                if data.dmc:
-                    raise RuntimeError("dedispersed archive: dededispersion needs PSRCHIVE")
-                if not len(data.ok_isubs):
+                arch = self._open(datafile, tscrunch, quiet)
+                meta = arch.meta
+                if not len(meta.ok_isubs):
                     if not quiet:
                         print("No subints to fit for %s.  Skipping it." % datafile)
                     continue
@@ -238,34 +291,49 @@ class GetTOAs:
                 if not quiet:
                     print("Cannot load_data(%s).  Skipping it." % datafile)
                 continue
-            name = datafile if isinstance(datafile, str) else data.filename
-            job = self._prepare(name, data, nu_refs, nu_fits, fit_scat, method, bounds, quiet)
+            name = datafile if isinstance(datafile, str) else meta.filename
+            job = self._prepare(name, meta, nu_refs, nu_fits, fit_scat, method, bounds, quiet)
             if job is not None:
+                job.arch = arch
                 jobs.append(job)
-        # 2. fit: the (archive, subint) units in get_TOAs order are split into
-        #    contiguous shards, one per rank (torch.distributed, one process per
-        #    GPU); no collective on the fit path
+        # 2. shard the units, read and fit this rank's subints
         rank, world = _dist_info()
-        units = [(ij, isub) for ij, job in enumerate(jobs) for isub in job.ok_isubs]
-        lo, hi = _shard_range(len(units), rank, world)
-        results, durations = self._fit_units(jobs, units[lo:hi], fit_scat, method)
-        # 3. gather every rank's per-subint results (small host dicts), then
-        #    every rank assembles the same TOAs in the reference's order
+        counts = [len(j.ok_isubs) for j in jobs]
+        lo, hi = _shard_range(int(sum(counts)), rank, world)
+        parts, durations, off = {}, {}, 0
+        for ij, job in enumerate(jobs):
+            a0, a1 = max(lo, off) - off, min(hi, off + counts[ij]) - off
+            off += counts[ij]
+            if a1 <= a0:
+                continue
+            t0 = time.time()
+            parts[ij] = (a0, self._fit_job(job, a0, a1, fit_scat, method))
+            durations[ij] = time.time() - t0
+        # 3. gather every rank's result rows; every rank assembles all TOAs
         if world > 1:
             import torch.distributed as dist
-            parts = [None] * world
-            dist.all_gather_object(parts, (results, durations))
-            results, durations = {}, {}
-            for res_r, dur_r in parts:
-                results.update(res_r)
-                for ij, t in dur_r.items():
+            got = [None] * world
+            dist.all_gather_object(got, (parts, durations))
+            parts, durations = {}, {}
+            for p_r, d_r in got:
+                for ij, v in p_r.items():
+                    parts.setdefault(ij, []).append(v)
+                for ij, t in d_r.items():
                     durations[ij] = durations.get(ij, 0.0) + t
-        for ij, job in enumerate(jobs):
-            res_all = {isub: results[(ij, isub)] for isub in job.ok_isubs}
-            self._assemble(job.name, job.data, job.obs, job.DM0, job.MJDs, job.ok_isubs,
-                           job.fit_flags_sub, res_all, job.nu_fits_a, job.nu_refs_a,
-                           job.models, job.midx, print_phase, print_flux, print_parangle,
-                           addtnl_toa_flags, durations.get(ij, 0.0), quiet)
+        else:
+            parts = {ij: [v] for ij, v in parts.items()}
+        gc_on = gc.isenabled()
+        gc.disable()  # a few containers per TOA: keep the cyclic collector out of assembly
+        try:
+            for ij, job in enumerate(jobs):
+                pieces = sorted(parts[ij], key=lambda v: v[0])
+                res = pieces[0][1] if len(pieces) == 1 else \
+                    {k: np.concatenate([p[1][k] for p in pieces]) for k in pieces[0][1]}
+                self._assemble(job, res, print_phase, print_flux, print_parangle,
+                               addtnl_toa_flags, durations.get(ij, 0.0), quiet)
+        finally:
+            if gc_on:
+                gc.enable()
         tot = time.time() - start
         if not quiet and len(self.ok_isubs):
             n = np.array([len(x) for x in self.ok_isubs]).sum()
@@ -310,11 +378,7 @@ class GetTOAs:
         from .engine import get_engine
         for iarch, datafile in enumerate(datafiles):
             try:
-                data = _arch.load_data(datafile, dedisperse=False, dededisperse=False,
-                                       tscrunch=tscrunch, pscrunch=True, rm_baseline=rm_baseline,
-                                       quiet=quiet)
-                if data.dmc:
-                    raise RuntimeError("dedispersed archive: dededispersion needs PSRCHIVE")
+                data = self._load(datafile, tscrunch, quiet, rm_baseline)
                 if not len(data.ok_isubs):
                     if not quiet:
                         print("No subints to fit for %s.  Skipping it." % datafile)
@@ -331,8 +395,7 @@ class GetTOAs:
             MJDs = np.array([data.epochs[i].in_days() for i in range(nsub)], dtype=np.double)
             mweights = None
             if self.is_FITS_model:
-                md = _arch.load_data(self.modelfile)
-                model = np.asarray((md.masks * md.subints)[0, 0])
+                md, model = self._fits_model()
                 if md.nbin != nbin:
                     if not quiet:
                         print("Model nbin %d != data nbin %d for %s; skipping it." % (
@@ -468,11 +531,7 @@ class GetTOAs:
         ifile = ok_files.index(datafile)
         # rm_baseline=True as in show_fit; archives reach this build already
         # loaded (PSRCHIVE's baseline removal is out of scope, archive.py)
-        data = _arch.load_data(datafile, dedisperse=False, dededisperse=False,
-                               tscrunch=getattr(self, "tscrunch", False), pscrunch=True,
-                               rm_baseline=True, quiet=quiet)
-        if data.dmc:
-            raise RuntimeError("dedispersed archive: dededispersion needs PSRCHIVE")
+        data = self._load(datafile, getattr(self, "tscrunch", False), quiet, True)
         nbin = data.nbin
         irf = self._irf_active()
         spline = None
@@ -501,10 +560,7 @@ class GetTOAs:
             if key not in mkeys:
                 mkeys[key] = len(models)
                 if self.is_FITS_model:
-                    md = _arch.load_data(self.modelfile)
-                    m = np.asarray((md.masks * md.subints)[0, 0])
-                    if md.nchan == 1:
-                        m = np.tile(m[0], len(freqs)).reshape(len(freqs), md.nbin)
+                    md, m = self._fits_model(len(freqs))
                 elif tau != 0.0:
                     info = read_model(self.modelfile, quiet=True)
                     gparams = np.copy(info[4])
@@ -644,13 +700,15 @@ class GetTOAs:
 
     def _prepare(self, datafile, data, nu_ref_tuple, nu_fit_tuple, fit_scat, method, bounds,
                  quiet):
-        """Per-archive set-up of pptoas.py:246-484: templates, reference
-        frequencies, initial parameters and the per-subint fit flags."""
+        """Per-archive set-up of pptoas.py:246-484 on the metadata, as arrays:
+        templates, reference frequencies, initial parameters and the
+        per-subint fit flags."""
         nsub, nchan, nbin = data.nsub, data.nchan, data.nbin
         obs = DataBunch(telescope=data.telescope, backend=data.backend, frontend=data.frontend)
         DM_stored = data.DM
         DM0 = DM_stored if self.DM0 is None else self.DM0
-        MJDs = np.array([data.epochs[i].in_days() for i in range(nsub)], dtype=np.double)
+        ep = data.get("epoch_parts") or epoch_parts(data.epochs)
+        MJDs = ep[0] + (ep[1] + ep[2]) / 86400.0  # MJD.in_days elementwise
         ok_isubs = np.asarray(data.ok_isubs)
         mm = self._models(data, fit_scat, quiet)
         if mm is None:
@@ -660,112 +718,167 @@ class GetTOAs:
         models, midx, _ = mm
         if self._irf_active():
             models, midx = self._irf_models(models, midx, data, ok_isubs)
-        mask = np.zeros((nsub, nchan), dtype=np.uint8)
-        for isub in ok_isubs:
-            mask[isub, data.ok_ichans[isub]] = 1
-        # per-subint reference frequencies, guesses and flag sets (pptoas.py:383-484)
+        wn = np.asarray(data.weights) != 0.0
+        mask = wn.astype(np.uint8)
+        nchx = wn.sum(axis=1)
+        allok = nchx == nchan
+        # reference frequencies (pptoas.py:396-415)
         nu_fits_a = np.zeros((nsub, 3))
+        if nu_fit_tuple is None:
+            nu_fits_a[ok_isubs] = self._guess_fit_freqs(data, ok_isubs, wn, allok)[:, None]
+        else:
+            nu_fits_a[ok_isubs] = [nu_fit_tuple[0], nu_fit_tuple[0], nu_fit_tuple[-1]]
         nu_refs_a = np.full((nsub, 3), np.nan)
+        if nu_ref_tuple is not None:
+            nu_refs_a[ok_isubs] = [nu_ref_tuple[0], nu_ref_tuple[0], nu_ref_tuple[-1]]
+            if self.bary and nu_ref_tuple[-1]:
+                nu_refs_a[ok_isubs, 2] /= np.asarray(data.doppler_factors)[ok_isubs]
+        # initial guesses (pptoas.py:420-456; phi from the device guess)
         init = np.zeros((nsub, 5))
         guess_tau = np.zeros(nsub)
-        fit_flags_sub = {}
-        for isub in ok_isubs:
-            ok = data.ok_ichans[isub]
-            freqsx = data.freqs[isub, ok]
-            P = data.Ps[isub]
-            if nu_fit_tuple is None:
-                nu_fit = guess_fit_freq(freqsx, data.SNRs[isub, 0, ok])
-                nu_fits_a[isub] = [nu_fit] * 3
+        init[ok_isubs, 1] = DM_stored
+        if fit_scat:
+            P = data.Ps[ok_isubs]
+            nu_fit_tau = nu_fits_a[ok_isubs, 2]
+            if self.scat_guess is not None:
+                ts, tref, alpha_g = self.scat_guess
+                tau_g = (ts / P) * (nu_fit_tau / tref) ** alpha_g
             else:
-                nu_fits_a[isub] = [nu_fit_tuple[0], nu_fit_tuple[0], nu_fit_tuple[-1]]
-            if nu_ref_tuple is not None:
-                nu_refs_a[isub] = [nu_ref_tuple[0], nu_ref_tuple[0], nu_ref_tuple[-1]]
-                if self.bary and nu_ref_tuple[-1]:
-                    nu_refs_a[isub, 2] /= data.doppler_factors[isub]
-            tau_g = alpha_g = 0.0
-            if fit_scat:
-                nu_fit_tau = nu_fits_a[isub, 2]
-                if self.scat_guess is not None:
-                    ts, tref, alpha_g = self.scat_guess
-                    tau_g = (ts / P) * (nu_fit_tau / tref) ** alpha_g
+                alpha_g = self.alpha if hasattr(self, "alpha") else scattering_alpha
+                tau_g = (self.gparams[1] / P) * (nu_fit_tau / self.model_nu_ref) ** alpha_g \
+                    if hasattr(self, "gparams") else np.zeros(len(ok_isubs))
+            tau_g = np.asarray(tau_g, dtype=np.float64) * np.ones(len(ok_isubs))
+            guess_tau[ok_isubs] = tau_g
+            if self.log10_tau:
+                tau_g = np.log10(np.where(tau_g == 0.0, nbin ** -1, tau_g))
+            init[ok_isubs, 3] = tau_g
+            init[ok_isubs, 4] = alpha_g
+        # per-subint fit flags (pptoas.py:474-484): get_TOAs keeps one
+        # fit_flags list across subints and archives, and a 2-channel subint
+        # (fit_DM and fit_GM) zeroes GM in the *previous* subint's list --
+        # phase-only after a 1-channel subint, and an UnboundLocalError when no
+        # subint came before it.
+        ff_all = np.zeros((nsub, 5), dtype=np.int64)
+        special = (nchx[ok_isubs] == 1) | ((nchx[ok_isubs] == 2) & bool(self.fit_DM and self.fit_GM))
+        if not special.any():
+            ff_all[ok_isubs] = self.fit_flags
+            self._fit_flags_prev = list(self.fit_flags)
+        else:
+            for isub in ok_isubs:
+                n = nchx[isub]
+                if n == 1:
+                    ff = [1, 0, 0, 0, 0]
+                elif n == 2 and self.fit_DM and self.fit_GM:
+                    if self._fit_flags_prev is None:
+                        raise UnboundLocalError(
+                            "local variable 'fit_flags' referenced before assignment")
+                    ff = list(self._fit_flags_prev)
+                    ff[2] = 0
                 else:
-                    alpha_g = self.alpha if hasattr(self, "alpha") else scattering_alpha
-                    tau_g = (self.gparams[1] / P) * (nu_fit_tau / self.model_nu_ref) ** alpha_g \
-                        if hasattr(self, "gparams") else 0.0
-                guess_tau[isub] = tau_g
-                if self.log10_tau:
-                    if tau_g == 0.0:
-                        tau_g = nbin ** -1
-                    tau_g = np.log10(tau_g)
-            init[isub] = [0.0, DM_stored, 0.0, tau_g, alpha_g]
-            # pptoas.py:474-484 verbatim in effect: get_TOAs keeps one
-            # fit_flags list across subints and archives, and a 2-channel
-            # subint (fit_DM and fit_GM) zeroes GM in the *previous* subint's
-            # list -- phase-only after a 1-channel subint, and an
-            # UnboundLocalError when no subint came before it.
-            if len(freqsx) == 1:
-                ff = [1, 0, 0, 0, 0]
-            elif len(freqsx) == 2 and self.fit_DM and self.fit_GM:
-                if self._fit_flags_prev is None:
-                    raise UnboundLocalError(
-                        "local variable 'fit_flags' referenced before assignment")
-                ff = list(self._fit_flags_prev)
-                ff[2] = 0
-            else:
-                ff = list(self.fit_flags)
-            self._fit_flags_prev = ff
-            fit_flags_sub[isub] = ff
+                    ff = list(self.fit_flags)
+                self._fit_flags_prev = ff
+                ff_all[isub] = ff
         if bounds is None and method == "TNC":
             # get_TOAs' default TNC bounds (pptoas.py:458-467)
             bounds = [(None, None), (None, None), (None, None),
                       (np.log10((10 * nbin) ** -1), None) if self.log10_tau else (0.0, None),
                       (-10.0, 10.0)]
-        return DataBunch(name=datafile, data=data, obs=obs, DM0=DM0, MJDs=MJDs,
-                         ok_isubs=ok_isubs, models=models, midx=midx, mask=mask,
-                         nu_fits_a=nu_fits_a, nu_refs_a=nu_refs_a, init=init,
-                         guess_tau=guess_tau, fit_flags_sub=fit_flags_sub, bounds=bounds)
+        return DataBunch(name=datafile, data=data, obs=obs, DM0=DM0, MJDs=MJDs, epoch_parts=ep,
+                         ok_isubs=ok_isubs, models=models, midx=midx, mask=mask, wn=wn,
+                         nchx=nchx, nu_fits_a=nu_fits_a, nu_refs_a=nu_refs_a, init=init,
+                         guess_tau=guess_tau, ff=ff_all, bounds=bounds)
 
-    def _fit_units(self, jobs, units, fit_scat, method):
-        """Fit this rank's (archive, subint) units: one batched device call per
-        archive and flag set.  Returns {(archive, subint): one-row result dict}
-        and the fit wall time per archive."""
-        results, durations = {}, {}
-        by_arch = {}
-        for ij, isub in units:
-            by_arch.setdefault(ij, []).append(isub)
-        for ij, subs_all in by_arch.items():
-            job = jobs[ij]
-            data = job.data
-            subints = np.asarray(data.subints)[:, 0]
-            errs = None if data.get("noise_stds") is None else data.noise_stds[:, 0]
-            flag_sets = {}
-            for isub in subs_all:
-                flag_sets.setdefault(tuple(job.fit_flags_sub[isub]), []).append(isub)
-            for ff, subs in flag_sets.items():
-                subs = np.array(subs)
-                t0 = time.time()
-                # errs None: the device estimates get_noise_PS per channel,
-                # as load_data's noise_stds (pplib.py:2744-2748)
-                res = fit_portraits_batch(
-                    subints[subs], job.models, job.init[subs], data.Ps[subs], data.freqs[subs],
-                    nu_fits=job.nu_fits_a[subs], nu_outs=job.nu_refs_a[subs],
-                    errs=None if errs is None else errs[subs], fit_flags=list(ff),
-                    log10_tau=self.log10_tau, option=0, is_toa=True,
-                    chan_mask=job.mask[subs], weights=data.weights[subs],
-                    model_idx=job.midx[subs], guess=True, guess_Ns=100, guess_wrap=True,
-                    guess_nu=None, guess_tau=job.guess_tau[subs] if fit_scat else None,
-                    method=method, bounds=job.bounds)
-                durations[ij] = durations.get(ij, 0.0) + time.time() - t0
-                for j, isub in enumerate(subs):
-                    results[(ij, int(isub))] = {k: np.asarray(v)[j:j + 1] for k, v in res.items()}
-        return results, durations
+    @staticmethod
+    def _guess_fit_freqs(data, ok_isubs, wn, allok):
+        """guess_fit_freq(freqsx, SNRsx) of every ok subint (pptoas.py:401,
+        pplib.py:2618-2632): whole rows at once where every channel is on
+        (numpy's row sums are its 1-D sums), the compressed rows otherwise."""
+        f = data.freqs[ok_isubs]
+        snr = np.asarray(data.SNRs)[ok_isubs, 0]
+        if allok[ok_isubs].all() and (f == f[0]).all() and (snr == snr[0]).all():
+            return np.full(len(ok_isubs), guess_fit_freq(f[0], snr[0]))  # one distinct row
+        nu0 = (f.min(axis=1) + f.max(axis=1)) * 0.5
+        f2 = f ** -2
+        out = nu0 + np.sum((f - nu0[:, None]) * snr * f2, axis=1) / np.sum(snr * f2, axis=1)
+        for j in np.flatnonzero(~allok[ok_isubs]):
+            isub = ok_isubs[j]
+            ok = wn[isub]
+            out[j] = guess_fit_freq(data.freqs[isub, ok], np.asarray(data.SNRs)[isub, 0, ok])
+        return out
 
-    def _assemble(self, datafile, data, obs, DM0, MJDs, ok_isubs, fit_flags_sub, res_all,
-                  nu_fits_a, nu_refs_a, models, midx, print_phase, print_flux,
-                  print_parangle, addtnl_toa_flags, fit_duration, quiet):
-        """Host bookkeeping of pptoas.py:522-720 from the device results."""
+    def _fit_job(self, job, a0, a1, fit_scat, method):
+        """Fit ok subints job.ok_isubs[a0:a1] of one archive: read only their
+        subint range, then one batched device call per flag set.  Returns
+        result rows aligned with job.ok_isubs[a0:a1]."""
+        subs = job.ok_isubs[a0:a1]
+        data = job.data
+        s_lo, s_hi = int(subs[0]), int(subs[-1]) + 1
+        sub = job.arch.read(s_lo, s_hi)[:, 0]  # [s_hi - s_lo, nchan, nbin], numpy or device
+        ns = data.get("noise_stds")
+        errs = None if ns is None else np.asarray(ns)[:, 0]
+        ffs = job.ff[subs]
+        groups = [np.arange(len(subs))] if (ffs == ffs[0]).all() else \
+            [np.flatnonzero((ffs == r).all(axis=1)) for r in np.unique(ffs, axis=0)]
+        out = None
+        for g in groups:
+            s = subs[g]
+            rel = s - s_lo
+            if len(rel) == rel[-1] - rel[0] + 1:  # contiguous: a view
+                d = sub[int(rel[0]):int(rel[-1]) + 1]
+            else:
+                d = sub[rel] if not _arch._is_tensor(sub) else sub[_arch_index(rel, sub)]
+            # errs None: the device estimates get_noise_PS per channel, as
+            # load_data's noise_stds (pplib.py:2744-2748)
+            res = fit_portraits_batch(
+                d, job.models, job.init[s], data.Ps[s], data.freqs[s],
+                nu_fits=job.nu_fits_a[s], nu_outs=job.nu_refs_a[s],
+                errs=None if errs is None else errs[s], fit_flags=list(ffs[g[0]]),
+                log10_tau=self.log10_tau, option=0, is_toa=True,
+                chan_mask=job.mask[s], weights=data.weights[s],
+                model_idx=job.midx[s], guess=True, guess_Ns=100, guess_wrap=True,
+                guess_nu=None, guess_tau=job.guess_tau[s] if fit_scat else None,
+                method=method, bounds=job.bounds)
+            keep = {k: np.asarray(res[k]) for k in _RESULT_KEYS if k in res}
+            if len(groups) == 1:
+                return keep
+            if out is None:
+                out = {k: np.zeros((len(subs),) + v.shape[1:], dtype=v.dtype)
+                       for k, v in keep.items()}
+            for k, v in keep.items():
+                out[k][g] = v
+        return out
+
+    def _assemble(self, job, res, print_phase, print_flux, print_parangle, addtnl_toa_flags,
+                  fit_duration, quiet):
+        """Host bookkeeping of pptoas.py:522-720 from the device results, as
+        array operations; one TOA record per ok subint."""
+        data, datafile = job.data, job.name
         nsub, nchan, nbin = data.nsub, data.nchan, data.nbin
+        ok = job.ok_isubs
+        nok = len(ok)
         z = lambda *s: np.zeros(s, dtype=np.float64)
+        p, e = res["params"], res["param_errs"]
+        status, nfev = res["status"].astype(np.int64), res["nfev"].astype(np.int64)
+        for j in np.flatnonzero(~np.isin(status, (0, 1, 2, 4))):
+            report_failure(int(status[j]), "%s_%d" % (datafile, ok[j]))
+        ff = job.ff[ok]
+        P = data.Ps[ok]
+        phi, phi_err = p[:, 0], e[:, 0]
+        DM, DM_err, GM, GM_err = p[:, 1].copy(), e[:, 1], p[:, 2].copy(), e[:, 2]
+        toa_mjds = add_days(tuple(x[ok] for x in job.epoch_parts),
+                            ((phi * P) + data.backend_delay) / (3600 * 24.))
+        TOA_err = phi_err * P * 1e6
+        if self.bary:
+            df = np.asarray(data.doppler_factors, dtype=np.float64)[ok]
+            DM = np.where(ff[:, 1] != 0, DM * df, DM)
+            GM = np.where(ff[:, 2] != 0, GM * df ** 3, GM)
+        else:
+            df = np.ones(nok)
+        wn = job.wn[ok]
+        wall = bool(wn.all())
+        sc = res["scales"] if wall else np.where(wn, res["scales"], 0.0)
+        sce = res["scale_errs"] if wall else np.where(wn, res["scale_errs"], 0.0)
+        nuo = res["nu_out"]
         phis, phi_errs, DMs, DM_errs = z(nsub), z(nsub), z(nsub), z(nsub)
         GMs, GM_errs, taus, tau_errs = z(nsub), z(nsub), z(nsub), z(nsub)
         alphas, alpha_errs, snrs, red_chi2s = z(nsub), z(nsub), z(nsub), z(nsub)
@@ -777,120 +890,113 @@ class GetTOAs:
         rcs = np.zeros(nsub, dtype="int")
         TOAs = np.zeros(nsub, dtype="object")
         TOA_errs = np.zeros(nsub, dtype="object")
-        nu_fits = list(nu_fits_a)
-        nu_refs = [list(r) for r in nu_refs_a]
-        for isub in ok_isubs:
-            res, j = res_all[int(isub)], 0
-            ff = fit_flags_sub[isub]
-            ok = data.ok_ichans[isub]
-            freqsx = data.freqs[isub, ok]
-            P = data.Ps[isub]
-            p, e = res["params"][j], res["param_errs"][j]
-            phi, phi_err = p[0], e[0]
-            DM, DM_err, GM, GM_err = p[1], e[1], p[2], e[2]
-            report_failure(int(res["status"][j]), "%s_%d" % (datafile, isub))
-            toa_mjd = data.epochs[isub] + MJD(((phi * P) + data.backend_delay) / (3600 * 24.))
-            TOA_err = phi_err * P * 1e6
-            if self.bary:
-                df = data.doppler_factors[isub]
-                if ff[1]:
-                    DM *= df
-                if ff[2]:
-                    GM *= df ** 3
-            else:
-                df = 1.0
-            sc = res["scales"][j][ok]
-            sce = res["scale_errs"][j][ok]
-            if print_flux:
-                # scattering keeps each row's mean, so the scattered model's
-                # channel means are the template's (pptoas.py:553-575)
-                means = models[midx[isub]][ok].mean(axis=1)
-                pfl[isub, ok] = means * sc
-                pfle[isub, ok] = abs(means) * sce
-                fluxes[isub], flux_errs[isub] = weighted_mean(pfl[isub, ok], pfle[isub, ok])
-                flux_freqs[isub] = weighted_mean(freqsx, pfle[isub, ok])[0]
-            nuo = res["nu_out"][j]
-            nu_refs[isub] = [nuo[0], nuo[1], nuo[2]]
-            phis[isub], phi_errs[isub] = phi, phi_err
-            TOAs[isub], TOA_errs[isub] = toa_mjd, TOA_err
-            DMs[isub], DM_errs[isub], GMs[isub], GM_errs[isub] = DM, DM_err, GM, GM_err
-            taus[isub], tau_errs[isub] = p[3], e[3]
-            alphas[isub], alpha_errs[isub] = p[4], e[4]
-            nfevals[isub], rcs[isub] = res["nfev"][j], res["status"][j]
-            scales[isub, ok], scale_errs[isub, ok] = sc, sce
-            snrs[isub] = res["snr"][j]
-            chsnrs[isub, ok] = res["channel_snrs"][j][ok]
-            nf = int(np.sum(ff))
-            cm = res["cov"][j][:nf, :nf]
-            try:
-                covs[isub] = cm
-            except ValueError:
-                for ii, ifit in enumerate(np.where(ff)[0]):
-                    for jj, jfit in enumerate(np.where(ff)[0]):
-                        covs[isub][ifit, jfit] = cm[ii, jj]
-            red_chi2s[isub] = res["red_chi2"][j]
-            flags = {}
-            DM_out, DM_err_out = DM, DM_err
-            if not ff[1]:
-                DM_out = DM_err_out = None
-            if ff[2]:
-                flags["gm"] = GM
-                flags["gm_err"] = GM_err
-            if ff[3]:
-                if self.log10_tau:
-                    flags["scat_time"] = 10 ** p[3] * P / df * 1e6
-                    flags["log10_scat_time"] = p[3] + np.log10(P / df)
-                    flags["log10_scat_time_err"] = e[3]
-                else:
-                    flags["scat_time"] = p[3] * P / df * 1e6
-                    flags["scat_time_err"] = e[3] * P / df * 1e6
-                flags["scat_ref_freq"] = nuo[2] * df
-                flags["scat_ind"] = p[4]
-            if ff[4]:
-                flags["scat_ind_err"] = e[4]
-            flags["be"] = data.backend
-            flags["fe"] = data.frontend
-            flags["f"] = data.frontend + "_" + data.backend
-            flags["nbin"] = nbin
-            flags["nch"] = nchan
-            flags["nchx"] = len(freqsx)
-            flags["bw"] = freqsx.max() - freqsx.min()
-            flags["chbw"] = abs(data.bw) / nchan
-            flags["subint"] = int(isub)
-            flags["tobs"] = data.subtimes[isub]
-            flags["fratio"] = freqsx.max() / freqsx.min()
-            flags["tmplt"] = self.modelfile
-            flags["snr"] = res["snr"][j]
-            if not np.isnan(nu_refs_a[isub][0]) and np.all(ff[:2]):
-                flags["phi_DM_cov"] = cm[0, 1]
-            flags["gof"] = res["red_chi2"][j]
-            if print_phase:
-                flags["phs"] = phi
-                flags["phs_err"] = phi_err
-            if print_flux:
-                flags["flux"] = fluxes[isub]
-                flags["flux_err"] = flux_errs[isub]
-                flags["flux_ref_freq"] = flux_freqs[isub]
-            if print_parangle:
-                flags["par_angle"] = data.parallactic_angles[isub]
-            for k, v in addtnl_toa_flags.items():
-                flags[k] = v
-            self.TOA_list.append(TOA(datafile, nuo[0], toa_mjd, TOA_err, data.telescope,
-                                     data.telescope_code, DM_out, DM_err_out, flags))
+        phis[ok], phi_errs[ok] = phi, phi_err
+        TOAs[ok] = toa_mjds
+        TOA_errs[ok] = TOA_err
+        DMs[ok], DM_errs[ok], GMs[ok], GM_errs[ok] = DM, DM_err, GM, GM_err
+        taus[ok], tau_errs[ok] = p[:, 3], e[:, 3]
+        alphas[ok], alpha_errs[ok] = p[:, 4], e[:, 4]
+        nfevals[ok], rcs[ok] = nfev, status
+        scales[ok], scale_errs[ok] = sc, sce
+        snrs[ok] = res["snr"]
+        chsnrs[ok] = res["channel_snrs"] if wall else np.where(wn, res["channel_snrs"], 0.0)
+        red_chi2s[ok] = res["red_chi2"]
+        nf = ff.sum(axis=1)
+        cov = res["cov"]
+        full = nf == self.nfit
+        if full.all():
+            covs[ok] = cov[:, :self.nfit, :self.nfit]
+        else:
+            for j in range(nok):
+                cm = cov[j][:nf[j], :nf[j]]
+                try:  # the reference's assignment, broadcasting a 1x1 block
+                    covs[ok[j]] = cm
+                except ValueError:
+                    w = np.where(ff[j])[0]
+                    for ii, ifit in enumerate(w):
+                        for jj, jfit in enumerate(w):
+                            covs[ok[j]][ifit, jfit] = cm[ii, jj]
+        fo = data.freqs[ok]
+        fmax = (fo if wall else np.where(wn, fo, -np.inf)).max(axis=1)
+        fmin = (fo if wall else np.where(wn, fo, np.inf)).min(axis=1)
+        if print_flux:
+            # scattering keeps each row's mean, so the scattered model's
+            # channel means are the template's (pptoas.py:553-575)
+            for j, isub in enumerate(ok):
+                okc = wn[j]
+                means = job.models[job.midx[isub]][okc].mean(axis=1)
+                pfl[isub, okc] = means * sc[j][okc]
+                pfle[isub, okc] = abs(means) * sce[j][okc]
+                fluxes[isub], flux_errs[isub] = weighted_mean(pfl[isub, okc], pfle[isub, okc])
+                flux_freqs[isub] = weighted_mean(data.freqs[isub, okc], pfle[isub, okc])[0]
+        # TOA records: flags in the reference's insertion order (pptoas.py:606-661)
+        has_ref = ~np.isnan(job.nu_refs_a[ok, 0])
+        cols = {}
+        cols["gm"], cols["gm_err"] = GM, GM_err
+        if self.log10_tau:
+            cols["scat_time"] = 10 ** p[:, 3] * P / df * 1e6
+            cols["log10_scat_time"] = p[:, 3] + np.log10(P / df)
+            cols["log10_scat_time_err"] = e[:, 3]
+        else:
+            cols["scat_time"] = p[:, 3] * P / df * 1e6
+            cols["scat_time_err"] = e[:, 3] * P / df * 1e6
+        cols["scat_ref_freq"] = nuo[:, 2] * df
+        cols["scat_ind"] = p[:, 4]
+        cols["scat_ind_err"] = e[:, 4]
+        subt = np.asarray(data.subtimes, dtype=object)[ok]
+        common = [("be", [data.backend] * nok), ("fe", [data.frontend] * nok),
+                  ("f", [data.frontend + "_" + data.backend] * nok), ("nbin", [nbin] * nok),
+                  ("nch", [nchan] * nok), ("nchx", job.nchx[ok].tolist()),
+                  ("bw", (fmax - fmin).tolist()), ("chbw", [abs(data.bw) / nchan] * nok),
+                  ("subint", ok.tolist()), ("tobs", subt.tolist()),
+                  ("fratio", (fmax / fmin).tolist()), ("tmplt", [self.modelfile] * nok),
+                  ("snr", res["snr"].tolist())]
+        cov01 = cov[:, 0, 1].tolist()
+        gof = res["red_chi2"].tolist()
+        tail = []
+        if print_phase:
+            tail += [("phs", phi.tolist()), ("phs_err", phi_err.tolist())]
+        if print_flux:
+            tail += [("flux", fluxes[ok].tolist()), ("flux_err", flux_errs[ok].tolist()),
+                     ("flux_ref_freq", flux_freqs[ok].tolist())]
+        if print_parangle:
+            tail += [("par_angle", np.asarray(data.parallactic_angles)[ok].tolist())]
+        extra = list(addtnl_toa_flags.items())
+        # one key list per (fit flags, phi_DM_cov present) pattern
+        pat = ff * np.array([1, 2, 4, 8, 16])
+        pat = pat.sum(axis=1) * 2 + (has_ref & (ff[:, 0] != 0) & (ff[:, 1] != 0))
+        used = set()
+        if ff[:, 2].any():
+            used |= {"gm", "gm_err"}
+        if ff[:, 3].any():
+            used |= {"scat_time", "log10_scat_time", "log10_scat_time_err", "scat_time_err",
+                     "scat_ref_freq", "scat_ind"}
+        if ff[:, 4].any():
+            used.add("scat_ind_err")
+        colv = {k: np.asarray(v).tolist() for k, v in cols.items() if k in used}
+        toas = [None] * nok
+        self._make_toas(toas, pat, ff, colv, common, cov01, gof, tail, extra, datafile,
+                        data.telescope, data.telescope_code, nuo[:, 0].tolist(),
+                        toa_mjds, TOA_err.tolist(), DM.tolist(), DM_err.tolist())
+        self.TOA_list.extend(toas)
+        nu_fits = list(job.nu_fits_a)  # list(np.zeros([nsub, 3])) filled (pptoas.py:283,406)
+        nr = np.zeros((nsub, 3))  # pptoas.py:284, ok rows from the fit (:527-530)
+        nr[ok] = nuo
+        nu_refs = nr.tolist()
         # DeltaDM weighted mean per archive (pptoas.py:664-681)
-        DeltaDMs = DMs - DM0
-        ok = ok_isubs
-        w = DM_errs[ok] ** -2 if np.all(DM_errs[ok]) else np.ones(len(ok))
+        DeltaDMs = DMs - job.DM0
+        w = DM_errs[ok] ** -2 if np.all(DM_errs[ok]) else np.ones(nok)
         mean, wsum = np.average(DeltaDMs[ok], weights=w, returned=True)
         var = wsum ** -1
-        if len(ok) > 1:
+        if nok > 1:
             var *= np.sum(((DeltaDMs[ok] - mean) ** 2) * w) / (len(DeltaDMs[ok]) - 1)
-        for attr, val in [("order", datafile), ("obs", obs), ("doppler_fs", data.doppler_factors),
-                          ("nu0s", data.nu0), ("nu_fits", nu_fits), ("nu_refs", nu_refs),
-                          ("ok_isubs", ok_isubs), ("epochs", data.epochs), ("MJDs", MJDs),
-                          ("Ps", data.Ps), ("phis", phis), ("phi_errs", phi_errs),
-                          ("TOAs", TOAs), ("TOA_errs", TOA_errs), ("DM0s", DM0),
-                          ("DMs", DMs), ("DM_errs", DM_errs), ("DeltaDM_means", mean),
+        for attr, val in [("order", datafile), ("obs", job.obs),
+                          ("doppler_fs", data.doppler_factors), ("nu0s", data.nu0),
+                          ("nu_fits", nu_fits), ("nu_refs", nu_refs), ("ok_isubs", ok),
+                          ("epochs", data.epochs), ("MJDs", job.MJDs), ("Ps", data.Ps),
+                          ("phis", phis), ("phi_errs", phi_errs), ("TOAs", TOAs),
+                          ("TOA_errs", TOA_errs), ("DM0s", job.DM0), ("DMs", DMs),
+                          ("DM_errs", DM_errs), ("DeltaDM_means", mean),
                           ("DeltaDM_errs", var ** 0.5), ("GMs", GMs), ("GM_errs", GM_errs),
                           ("taus", taus), ("tau_errs", tau_errs), ("alphas", alphas),
                           ("alpha_errs", alpha_errs), ("scales", scales),
@@ -905,6 +1011,65 @@ class GetTOAs:
         if not quiet:
             print("--------------------------")
             print(datafile)
-            print("~%.4f sec/TOA" % (fit_duration / len(ok_isubs)))
-            print("Med. TOA error is %.3f us" % (np.median(phi_errs[ok_isubs]) *
+            print("~%.4f sec/TOA" % (fit_duration / nok))
+            print("Med. TOA error is %.3f us" % (np.median(phi_errs[ok]) *
                                                  data.Ps.mean() * 1e6))
+
+    def _make_toas(self, toas, pat, ff, colv, common, cov01, gof, tail, extra, name, tel, tcode,
+                   freq, toa_mjds, terr, dmo, dmeo):
+        """TOA records into toas[j], one key list per (fit flags, phi_DM_cov
+        present) pattern; flags in the reference's insertion order
+        (pptoas.py:606-661), then the additional flags."""
+        xk = [k for k, _ in extra]
+        xv = [v for _, v in extra]
+        for code in np.unique(pat).tolist():
+            rows = np.flatnonzero(pat == code).tolist()
+            f5 = ff[rows[0]]
+            keys = []
+            if f5[2]:
+                keys += ["gm", "gm_err"]
+            if f5[3]:
+                keys += (["scat_time", "log10_scat_time", "log10_scat_time_err"]
+                         if self.log10_tau else ["scat_time", "scat_time_err"])
+                keys += ["scat_ref_freq", "scat_ind"]
+            if f5[4]:
+                keys += ["scat_ind_err"]
+            vals = [colv[k] for k in keys]
+            keys += [k for k, _ in common]
+            vals += [v for _, v in common]
+            if code & 1:
+                keys.append("phi_DM_cov")
+                vals.append(cov01)
+            keys.append("gof")
+            vals.append(gof)
+            keys += [k for k, _ in tail]
+            vals += [v for _, v in tail]
+            if len(rows) != len(toas):
+                vals = [[v[j] for j in rows] for v in vals]
+            has_dm = bool(f5[1])
+            new = object.__new__
+            for j, row in zip(rows, zip(*vals)):
+                flags = dict(zip(keys, row))
+                if xk:
+                    flags.update(zip(xk, xv))
+                # TOA(name, freq, mjd, err, tel, tcode, DM, DM_err, flags) without the call
+                t = new(TOA)
+                t.archive = name
+                t.frequency = freq[j]
+                t.MJD = toa_mjds[j]
+                t.TOA_error = terr[j]
+                t.telescope = tel
+                t.telescope_code = tcode
+                t.DM = dmo[j] if has_dm else None
+                t.DM_error = dmeo[j] if has_dm else None
+                t.flags = flags
+                toas[j] = t
+
+
+_RESULT_KEYS = ["params", "param_errs", "nu_out", "cov", "scales", "scale_errs",
+                "channel_snrs", "chi2", "red_chi2", "snr", "nfev", "status"]
+
+
+def _arch_index(rel, t):
+    import torch
+    return torch.as_tensor(rel, device=t.device, dtype=torch.long)

@@ -178,64 +178,82 @@ def pscrunch_mode(npol, pol_type):
     return 1
 
 
-def load_psrfits(path, pscrunch=True, dededisperse=False, tscrunch=False, rm_baseline=False,
-                 quiet=True, engine=None):
-    """pplib.load_data (pplib.py:2650-2820) for a fold-mode PSRFITS archive."""
-    if dededisperse:
-        raise NotImplementedError("dededispersion needs PSRCHIVE")
-    from .engine import get_engine
-    import torch
-    f = PSRFITSFile(path)
-    try:
-        I = f.info
+class PSRFITSSource:
+    """A fold-mode PSRFITS archive as an archive.Archive source: the metadata
+    load_data returns (pplib.py:2670-2735, 2809-2819) without touching DATA,
+    and ``read(lo, hi)`` = subints lo:hi, raw samples read on the host
+    (ppfits_read_raw) and unpacked + pscrunched on the device
+    (ppf_unpack_subints) -- only the 8/16-bit samples cross PCIe."""
+    eager_noise = True  # load_data computes noise_stds (pplib.py:2740-2748)
+
+    def __init__(self, path, pscrunch=True):
+        self.f = PSRFITSFile(path)
+        f, I = self.f, self.f.info
         if f.nsub == 0:
+            f.close()
             raise PSRFITSError("%s: no subintegrations" % path)
-        meta = f.meta()
-        raw = f.raw()
-        pc = f.polyco() if not I.has_period else None
-    finally:
-        f.close()
-    nsub, npol, nchan, nbin = raw.shape
-    pmode = pscrunch_mode(npol, f.text("pol_type")) if pscrunch else 0
-    eng = engine or get_engine()
-    dev = eng.device
-    rd = torch.from_numpy(raw).to(dev)
-    scl = torch.from_numpy(meta["scl"]).to(dev)
-    offs = torch.from_numpy(meta["offs"]).to(dev)
-    npo = 1 if pmode else npol
-    sub = torch.empty((nsub, npo, nchan, nbin), dtype=torch.float64, device=dev)
-    eng._chk(eng.lib.ppf_unpack_subints(eng.ctx, nsub, npol, nchan, nbin, I.raw_type,
-                                        ctypes.c_void_p(rd.data_ptr()),
-                                        ctypes.c_void_p(scl.data_ptr()),
-                                        ctypes.c_void_p(offs.data_ptr()), pmode,
-                                        ctypes.c_void_p(sub.data_ptr())))
-    noise = eng.noise_rows(sub.reshape(-1, nbin)).reshape(nsub, npo, nchan)
-    subints = sub.cpu().numpy()
-    noise_stds = noise.cpu().numpy()
-    # epochs: STT_IMJD + (STT_SMJD + STT_OFFS + OFFS_SUB) / 86400
-    start = MJD(I.stt_imjd, int(I.stt_smjd), float(I.stt_offs) + (I.stt_smjd - int(I.stt_smjd)))
-    epochs = [start + float(meta["offs_sub"][i]) for i in range(nsub)]
-    if I.has_period:
-        Ps = meta["period"].copy()
-    elif pc is not None:
-        Ps = np.array([polyco_period(pc, e.in_days()) for e in epochs])
-    else:
-        raise PSRFITSError("%s: no PERIOD column and no POLYCO table" % path)
-    tel = f.text("telescope")
-    DM = I.dm if np.isfinite(I.dm) else (I.chan_dm if np.isfinite(I.chan_dm) else 0.0)
-    par = meta["par_ang"] if I.has_par_ang else np.zeros(nsub)
-    state = "Intensity" if (pmode or npol == 1) else f.text("pol_type")
-    bunch = dict(subints=subints, freqs=meta["freqs"], weights=meta["weights"], Ps=Ps,
-                 epochs=epochs, noise_stds=noise_stds, SNRs=np.ones((nsub, npo, nchan)),
-                 doppler_factors=np.ones(nsub), parallactic_angles=np.asarray(par, float),
-                 DM=float(DM), dmc=int(I.dedispersed), backend=f.text("backend"),
+        self.path = path
+        self.m = f.meta()
+        self.pc = f.polyco() if not I.has_period else None
+        self.pmode = pscrunch_mode(f.npol, f.text("pol_type")) if pscrunch else 0
+        self.npo = 1 if self.pmode else f.npol
+        self.period_at = None if self.pc is None else (lambda mjd: polyco_period(self.pc, mjd))
+
+    def meta(self):
+        from .archive import normalize
+        f, I, m = self.f, self.f.info, self.m
+        nsub = f.nsub
+        # epochs: STT_IMJD + (STT_SMJD + STT_OFFS + OFFS_SUB) / 86400
+        start = MJD(I.stt_imjd, int(I.stt_smjd), float(I.stt_offs) + (I.stt_smjd - int(I.stt_smjd)))
+        epochs = [start + float(m["offs_sub"][i]) for i in range(nsub)]
+        if I.has_period:
+            Ps = m["period"].copy()
+        elif self.pc is not None:
+            Ps = np.array([polyco_period(self.pc, e.in_days()) for e in epochs])
+        else:
+            raise PSRFITSError("%s: no PERIOD column and no POLYCO table" % self.path)
+        tel = f.text("telescope")
+        DM = I.dm if np.isfinite(I.dm) else (I.chan_dm if np.isfinite(I.chan_dm) else 0.0)
+        par = m["par_ang"] if I.has_par_ang else np.zeros(nsub)
+        state = "Intensity" if (self.pmode or f.npol == 1) else f.text("pol_type")
+        b = dict(nsub=nsub, npol=self.npo, nchan=f.nchan, nbin=f.nbin, freqs=m["freqs"],
+                 weights=m["weights"], Ps=Ps, epochs=epochs, noise_stds=None,
+                 SNRs=np.ones((nsub, self.npo, f.nchan)), doppler_factors=np.ones(nsub),
+                 parallactic_angles=np.asarray(par, float), DM=float(DM),
+                 dmc=int(I.dedispersed), baseline_removed=False, backend=f.text("backend"),
                  frontend=f.text("frontend"), backend_delay=float(I.be_delay), telescope=tel,
-                 telescope_code=TELESCOPE_CODES.get(tel.upper(), tel),
-                 bw=float(I.obsbw), nu0=float(I.obsfreq), subtimes=list(meta["tsubint"]),
-                 source=f.text("source") or "noname", state=state, filename=path)
-    if tscrunch:  # arch.tscrunch() (pplib.py:2700); the POLYCO gives P at the new epoch
-        from .archive import tscrunch as _tscrunch
-        bunch = _tscrunch(bunch, None if pc is None else (lambda mjd: polyco_period(pc, mjd)))
-    if not quiet:
-        print("\nReading data from %s on source %s..." % (path, bunch["source"]))
-    return bunch
+                 telescope_code=TELESCOPE_CODES.get(tel.upper(), tel), bw=float(I.obsbw),
+                 nu0=float(I.obsfreq), subtimes=list(m["tsubint"]),
+                 source=f.text("source") or "noname", state=state, filename=self.path)
+        return normalize(b, self.path, subints=False)
+
+    def read(self, lo, hi, engine=None):
+        from .engine import get_engine
+        import torch
+        f, I = self.f, self.f.info
+        n = hi - lo
+        raw = f.raw(lo, n)
+        eng = engine or get_engine()
+        dev = eng.device
+        rd = torch.from_numpy(raw).to(dev)
+        scl = torch.from_numpy(np.ascontiguousarray(self.m["scl"][lo:hi])).to(dev)
+        offs = torch.from_numpy(np.ascontiguousarray(self.m["offs"][lo:hi])).to(dev)
+        sub = torch.empty((n, self.npo, f.nchan, f.nbin), dtype=torch.float64, device=dev)
+        eng._chk(eng.lib.ppf_unpack_subints(eng.ctx, n, f.npol, f.nchan, f.nbin, I.raw_type,
+                                            ctypes.c_void_p(rd.data_ptr()),
+                                            ctypes.c_void_p(scl.data_ptr()),
+                                            ctypes.c_void_p(offs.data_ptr()), self.pmode,
+                                            ctypes.c_void_p(sub.data_ptr())))
+        sub._keep = (rd, scl, offs)
+        return sub
+
+    def close(self):
+        self.f.close()
+
+
+def load_psrfits(path, pscrunch=True, dedisperse=False, dededisperse=False, tscrunch=False,
+                 rm_baseline=False, quiet=True):
+    """pplib.load_data (pplib.py:2650-2820) for a fold-mode PSRFITS archive."""
+    from .archive import load_data
+    return load_data(path, pscrunch=pscrunch, dedisperse=dedisperse, dededisperse=dededisperse,
+                     tscrunch=tscrunch, rm_baseline=rm_baseline, quiet=quiet)

@@ -74,9 +74,16 @@ def make_archives():
     return names
 
 
-def run_get_toas(log):
-    from pulseportraiture_amd import pplib, pptoas, synth
+def run_get_toas(log, reads=None):
+    from pulseportraiture_amd import archive, pplib, pptoas, synth
     names = make_archives()
+    if reads is not None:  # every subint range a rank reads (pptoas.py:246,343 sharded)
+        orig = archive._Registered.read
+
+        def read(self, lo, hi):
+            reads.append((self.base.filename, lo, hi))
+            return orig(self, lo, hi)
+        archive._Registered.read = read
 
     def fit(*a, **k):
         k["log_calls"] = log
@@ -96,10 +103,12 @@ def _toas_worker(rank, world, port, out_dir):
     os.environ["MASTER_PORT"] = str(port)
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        log = []
-        lines, gt = run_get_toas(log)
+        log, reads = [], []
+        lines, gt = run_get_toas(log, reads)
+        subs = sorted((n, k) for n, lo, hi in reads for k in range(lo, hi))
         np.savez(os.path.join(out_dir, "toas%d.npz" % rank), lines=np.array(lines),
-                 nfit=sum(log), DeltaDM=np.array(gt.DeltaDM_means))
+                 nfit=sum(log), DeltaDM=np.array(gt.DeltaDM_means),
+                 read=np.array(["%s:%d" % x for x in subs]))
     finally:
         torch.distributed.destroy_process_group()
 
@@ -113,6 +122,10 @@ def test_get_toas_sharded_ws2_equals_single_process():
         r = [np.load(os.path.join(d, "toas%d.npz" % k)) for k in range(2)]
     assert int(r[0]["nfit"]) + int(r[1]["nfit"]) == 12  # disjoint shards cover all units
     assert int(r[0]["nfit"]) == 6 and int(r[1]["nfit"]) == 6
+    # each rank read only the subints of its own shard: disjoint, covering all
+    # 12 ok subints (archive 0's masked subint 1 sits inside rank 0's range)
+    r0, r1 = set(r[0]["read"]), set(r[1]["read"])
+    assert not (r0 & r1) and len(r0) + len(r1) <= 13 and len(r0 | r1) >= 12
     for rk in r:
         assert list(rk["lines"]) == ref_lines  # same TOAs, same order, on every rank
         np.testing.assert_array_equal(rk["DeltaDM"], np.array(gt.DeltaDM_means))
@@ -146,8 +159,10 @@ def run_align():
     engine.get_engine = lambda device=None: NumpyEngine()
     ppalign.fit_portraits_batch = fake_fit
     w = synth.make_workload(1, 8, 64, seed=50)
+    # dmc=1: the registered guess is what load_data(dedisperse=True) returns
     archive.register_archive("dist_guess.npz", dict(subints=w.model[None, None], freqs=w.freqs,
-                                                    Ps=[w.P], epochs=[(57000, 0, 0.0)], DM=DM0))
+                                                    Ps=[w.P], epochs=[(57000, 0, 0.0)], DM=DM0,
+                                                    dmc=1))
     return ppalign.align_archives(names, "dist_guess.npz", fit_dm=True, niter=2, quiet=True)
 
 

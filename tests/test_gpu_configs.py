@@ -126,8 +126,10 @@ def test_align_archives_config5_shape(gpu):
         register_synth_archive(nm, 1, nchan, nbin, seed + i, 0.0, 0.0)
     w = synth.make_workload(1, nchan, nbin, seed=seed)
     guess = O.rotate_data(w.model, float(z["cfg_guess_rot"]))
+    # dmc=1: the fixture's guess is what load_data(dedisperse=True) returned
     archive.register_archive("guess5.fits", dict(subints=guess[None, None], freqs=w.freqs,
-                                                 Ps=[w.P], epochs=[(57300, 0, 0.0)], DM=DM0))
+                                                 Ps=[w.P], epochs=[(57300, 0, 0.0)], DM=DM0,
+                                                 dmc=1))
     k = np.arange(nbin)
     for niter in (1, 2):
         port = ppalign.align_archives(names, "guess5.fits", fit_dm=True, niter=niter,

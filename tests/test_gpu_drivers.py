@@ -142,8 +142,9 @@ def test_align_archives_golden(gpu):
     z = np.load(os.path.join(GOLDEN, "align.npz"))
     names = [str(n) for n in z["names"]]
     register_golden_archives(z, names)
+    # dmc=1: the fixture's guess is what load_data(dedisperse=True) returned
     guess = dict(subints=z["guess"][None, None], freqs=z["freqs"], Ps=[float(z["P"])],
-                 epochs=[(57202, 0, 0.0)], DM=DM0)
+                 epochs=[(57202, 0, 0.0)], DM=DM0, dmc=1)
     archive.register_archive("guess.fits", guess)
     for niter in (1, 2):
         port = ppalign.align_archives(names, "guess.fits", fit_dm=True, niter=niter, quiet=True)

@@ -50,7 +50,7 @@ def test_load_psrfits_unpack(gpu, tmp_path, pol_type):
     from pulseportraiture_amd import archive
     path = str(tmp_path / "c.fits")
     w, raw, scl, offs, wts = _coherence_archive(path, pol_type=pol_type)
-    d = archive.load_data(path, pscrunch=True)
+    d = archive.load_data(path, pscrunch=True, rm_baseline=False)
     phys = raw.astype(np.float64) * scl[..., None] + offs[..., None]
     want = phys[:, 0] + phys[:, 1] if pol_type == "AABBCRCI" else phys[:, 0]
     got = np.asarray(d.subints)[:, 0]
@@ -65,7 +65,7 @@ def test_load_psrfits_unpack(gpu, tmp_path, pol_type):
     np.testing.assert_allclose(d.Ps, w.P)
     assert abs(d.epochs[1].in_days() - (57300 + (43200 + 0.25 + 45.0) / 86400.0)) < 1e-12
     # unscrunched: all four polarisations
-    d4 = archive.load_data(path, pscrunch=False)
+    d4 = archive.load_data(path, pscrunch=False, rm_baseline=False)
     assert np.asarray(d4.subints).shape[1] == 4
 
 
@@ -73,7 +73,7 @@ def test_get_toas_psrfits_equals_registered(gpu, tmp_path):
     from pulseportraiture_amd import archive, pplib, pptoas, synth
     path = str(tmp_path / "t.fits")
     _coherence_archive(path, nsub=3, nchan=32, nbin=512, seed=21)
-    d = archive.load_data(path, pscrunch=True)
+    d = archive.load_data(path, pscrunch=True, rm_baseline=False)
     reg = {k: d[k] for k in ["subints", "freqs", "weights", "Ps", "epochs", "noise_stds",
                              "SNRs", "doppler_factors", "parallactic_angles", "DM", "dmc",
                              "backend", "frontend", "backend_delay", "telescope",
@@ -103,8 +103,8 @@ def test_tscrunch_psrfits_and_get_toas(gpu, tmp_path):
     from pulseportraiture_amd import archive, pplib, pptoas, synth
     path = str(tmp_path / "ts.fits")
     w, raw, scl, offs, wts = _coherence_archive(path, nsub=4, nchan=32, nbin=512, seed=31)
-    full = archive.load_data(path, pscrunch=True)
-    d = archive.load_data(path, pscrunch=True, tscrunch=True)
+    full = archive.load_data(path, pscrunch=True, rm_baseline=False)
+    d = archive.load_data(path, pscrunch=True, tscrunch=True, rm_baseline=False)
     sub = np.asarray(full.subints)[:, 0]
     ww = np.asarray(full.weights)
     want = np.einsum("sn,snj->nj", ww, sub) / ww.sum(0)[:, None]
