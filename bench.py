@@ -5,23 +5,30 @@ One step = the whole hot path over one batch of synthetic subints already
 resident in HBM: per-channel rfft + noise + cross-spectrum (k_data_xspec),
 the get_TOAs initial guess (k_guess: dedispersed average, brute force Ns=100,
 Nelder-Mead), Taylor moments of the cross-spectrum (k_moments) and the
-trust-ncg fit on them (k_fit_taylor) -- or, for scattering fits, the exact
-sweeps of k_solve -- and the post-fit (k_post: zero-covariance frequency,
-phi at nu_out, Woodbury covariance, snr, chi2), then the per-TOA results
-copied to the host.  Data: synthetic portraits from example.gmodel with
-injected phi/DM and sigma=1.5 Philox noise, generated on the device before
-timing.
+trust-ncg fit on them (k_fit_taylor) -- or, for scattering fits, the split
+exact sweeps (k_scat_sweep / k_scat_step) -- and the post-fit (k_post:
+zero-covariance frequency, phi at nu_out, Woodbury covariance, snr, chi2),
+then the per-TOA results copied to the host.  Data: synthetic portraits from
+example.gmodel with injected phi/DM and sigma=1.5 Philox noise, generated on
+the device before timing.
 
 N>1: launched by torch.distributed.run, one rank per GPU; each rank fits its
 own nsub subints (weak scaling, no collective on the fit path).  value =
 all ranks' TOAs / max-over-ranks time.
 
-Also reported: roofline of the dominant kernel (HIP-event timed on the
-stream it runs on) and the CPU baseline (the oracle restatement, 1 core) on a
-bounded sample of the same subints, plus the sample's parity vs the oracle.
+Beside value (N = 1, default config): the legs a caller actually gets --
+``get_toas`` (GetTOAs.get_TOAs end to end on a registered 10k-subint archive,
+TOA records and .tim text included; device-resident and host-resident input)
+and ``ppalign`` (align_archives at config 5, 4096 archives x 256 x 2048,
+niter 3).  Also reported: the roofline of the dominant kernel (HIP-event
+timed on the stream it runs on) and the CPU baseline (the oracle restatement,
+one process per available host core) on a bounded sample of the same
+workload, with the oracle/reference time ratio measured in the build
+container per config (tests/golden/timing_r3.json).
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -39,23 +46,36 @@ CONFIGS = {
                    "config 3: 1000 subints x 512 chan x 1024 bin, phase+DM+tau+alpha (log10 tau)"),
     "gm": (2000, 128, 2048, [1, 1, 1, 0, 0], 0.0, False, 0.0,
            "config 4 slice: 128 chan x 2048 bin, phase+DM+GM (per-GPU shard batch)"),
+    "get_toas": (10000, 64, 2048, [1, 1, 0, 0, 0], 0.0, False, 0.0,
+                 "GetTOAs.get_TOAs end to end: registered 10000 x 64 x 2048 archive, "
+                 "TOA records + .tim text"),
+    "ppalign": (4096, 256, 2048, [1, 1, 0, 0, 0], 0.0, False, 0.0,
+                "config 5: align_archives, 4096 archives x 256 chan x 2048 bin, niter 3"),
 }
+TIMING_KEY = {"headline": "headline", "get_toas": "headline", "gm": "gm",
+              "scattering": "scattering", "ppalign": "ppalign"}
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 FP64_PEAK_TFLOPS = 78.6  # AMD MI355X spec, fp64 vector = fp64 matrix (not in the guide's table)
-# HBM bytes per subint per kernel from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
-# passes over this same bench (tools/profile_r1.sh + tools/pmc_summary.py).
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
-KERNEL_SYMBOL = {"solve": "k_solve<false>", "data_xspec": "k_data_xspec<10>",
+# HBM bytes per launch per kernel from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
+# passes over this same bench (tools/profile_r03.sh + tools/pmc_summary.py)
+PMC_TRAFFIC = {"headline": os.path.join(ROOT, "profiles", "r03_pmc_traffic_headline.json"),
+               "scattering": os.path.join(ROOT, "profiles", "r03_pmc_traffic_scattering.json")}
+KERNEL_SYMBOL = {"solve": "k_scat_sweep", "data_xspec": "k_data_xspec<10>",
                  "post": "k_post<false>", "guess": "k_guess_w", "moments": "k_moments<4>",
                  "fit_taylor": "k_fit_taylor"}
+# fp64 operations of one scattering cell evaluation as cells_scat forms them
+# (ppfit_fit.hip: phasor step 6, W 6, B 13, f 8, g1 9, three conjugate
+# products 18, ten accumulations 30; the hardware reciprocal not counted)
+SCAT_FLOPS_PER_CELL = 90.0
 
 
-def pmc_traffic(kernel, nsub, nbin, nchan, config):
-    """Counter-measured HBM bytes per launch for the headline config, else None."""
-    if config != "headline" or nbin != 2048 or nchan != 64 or not os.path.exists(PMC_TRAFFIC):
+def pmc_traffic(kernel, nsub, config):
+    """Counter-measured HBM bytes per subint x nsub for this config, else None."""
+    f = PMC_TRAFFIC.get(config)
+    if f is None or not os.path.exists(f):
         return None
-    rec = json.load(open(PMC_TRAFFIC))
+    rec = json.load(open(f))
     k = rec["kernels"].get(KERNEL_SYMBOL.get(kernel, ""))
     if k is None:
         return None
@@ -72,16 +92,191 @@ def parse():
     ap.add_argument("--seed", type=int, default=20240917)
     ap.add_argument("--cpu-sample", type=int, default=None,
                     help="subints the 1-core oracle fits (default per config; 0: skip)")
-    ap.add_argument("--cpu-procs", type=int, default=16,
-                    help="processes (one per core) of the all-core CPU baseline")
-    ap.add_argument("--cpu-seconds", type=float, default=24.0,
-                    help="approximate CPU work (core-seconds, summed over the processes) "
-                         "of the all-core leg")
+    ap.add_argument("--cpu-procs", type=int, default=None,
+                    help="processes of the all-core CPU baseline (default: every core of "
+                         "os.sched_getaffinity within the cgroup CPU quota)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="CPU work per process of the all-core leg (s)")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP events")
+    ap.add_argument("--no-legs", action="store_true",
+                    help="headline only: skip the get_toas / ppalign legs")
+    ap.add_argument("--ppalign-narch", type=int, default=4096)
+    ap.add_argument("--ppalign-niter", type=int, default=3)
     ap.add_argument("--host-stream", type=int, default=None,
                     help="also time host-resident (pinned) input streamed over PCIe in chunks "
                          "of this many subints (default: on for config gm; 0: off)")
     return ap.parse_args()
+
+
+def host_cores():
+    """(cores to use, affinity count, cgroup quota in cores or None)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(p)
+    except (OSError, ValueError):
+        pass
+    n = aff if quota is None else max(1, min(aff, int(math.floor(quota))))
+    return n, aff, quota
+
+
+def timing_ratio(config):
+    f = os.path.join(ROOT, "tests", "golden", "timing_r3.json")
+    if not os.path.exists(f):
+        return None
+    rec = json.load(open(f)).get(TIMING_KEY.get(config, config))
+    return None if rec is None else rec["ratio_oracle_over_reference"]
+
+
+def synth_inputs(eng, config, nsub, seed, sub0):
+    """Synthetic subints of a config on the device + the fit arguments."""
+    import torch
+    from pulseportraiture_amd import synth, pplib
+    _, nchan, nbin, flags, tau, log10_tau, gm, _ = CONFIGS[config]
+    dev = eng.device
+    w = synth.make_workload(nsub, nchan, nbin, seed=seed, sub0=sub0, tau=tau, gm=gm)
+    data = eng.synth(w.template, w.phase, w.sigma, w.seed, sub0=w.sub0)
+    nu_fit = pplib.guess_fit_freq(w.freqs)  # SNR weights = 1 (SURVEY §8(d))
+    tau_g = 0.0
+    init_row = [0.0, w.DM0, 0.0, 0.0, 0.0]
+    if flags[3]:
+        # pptoas scattering guess: tau at nu_fit from the injected reference value
+        tau_g = tau * (nu_fit / w.nu_ref) ** w.alpha
+        init_row[3] = np.log10(tau_g) if log10_tau else tau_g
+        init_row[4] = w.alpha
+    kw = dict(model=torch.as_tensor(w.model, device=dev),
+              freqs=torch.as_tensor(w.freqs, device=dev),
+              P=torch.full((nsub,), w.P, dtype=torch.float64, device=dev),
+              init=torch.tensor([init_row] * nsub, dtype=torch.float64, device=dev),
+              nu=torch.full((nsub, 3), nu_fit, dtype=torch.float64, device=dev),
+              gtau=torch.full((nsub,), tau_g, dtype=torch.float64, device=dev)
+              if flags[3] else None)
+    return w, data, kw, tau_g
+
+
+# ---------------------------------------------------------------------------
+# legs beside value: get_TOAs end to end, align_archives at config 5
+# ---------------------------------------------------------------------------
+def leg_get_toas(eng, w, data, reps=3, host=False):
+    """GetTOAs(...).get_TOAs() + the .tim text of every TOA on a registered
+    archive holding the bench's own subints (device tensor, or host numpy for
+    the PCIe-inclusive variant)."""
+    import torch
+    from pulseportraiture_amd import archive, pplib, pptoas, synth
+    from pulseportraiture_amd.mjd import MJD
+    nsub = data.shape[0]
+    sub = data.cpu().numpy()[:, None] if host else data[:, None]
+    name = "bench_get_toas_host" if host else "bench_get_toas"
+    archive.register_archive(name, dict(
+        subints=sub, freqs=w.freqs, Ps=np.full(nsub, w.P), DM=w.DM0, telescope="GBT",
+        telescope_code="gb", backend="bench", frontend="synth",
+        epochs=[MJD(57000, int(30 * k), 0.0) for k in range(nsub)]))
+    times = []
+    lines = gt = None
+    for r in range(reps + 1):  # the first call is the warm-up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        gt = pptoas.GetTOAs([name], synth.EXAMPLE_GMODEL, quiet=True)
+        gt.get_TOAs(quiet=True)
+        lines = [pplib.toa_line(t) for t in gt.TOA_list]
+        t1 = time.perf_counter()
+        if r:
+            times.append(t1 - t0)
+    archive.unregister_archive(name)
+    t = float(np.median(times))
+    out = {"value": round(nsub / t, 1), "unit": "TOAs/s", "ms_per_call": round(t * 1e3, 2),
+           "calls": reps, "tim_lines": len(lines),
+           "input": "host numpy, streamed through pinned buffers (PCIe-inclusive)" if host
+           else "device tensor (HBM-resident)"}
+    return out, gt
+
+
+def leg_ppalign(eng, narch, niter, seed):
+    """align_archives over narch registered single-subint archives of config
+    5's shape (views of one device tensor), niter iterations."""
+    import torch
+    from pulseportraiture_amd import archive, ppalign, synth
+    _, nchan, nbin, _, _, _, _, _ = CONFIGS["ppalign"]
+    w = synth.make_workload(narch, nchan, nbin, seed=seed + 555)
+    data = eng.synth(w.template, w.phase, w.sigma, w.seed, sub0=w.sub0)
+    torch.cuda.synchronize()
+    names = []
+    for i in range(narch):
+        nm = "bench_pa_%d" % i
+        archive.register_archive(nm, dict(subints=data[i:i + 1, None], freqs=w.freqs, Ps=[w.P],
+                                          epochs=[(57000 + i, 0, 0.0)], DM=w.DM0))
+        names.append(nm)
+    # the initial guess: the template itself, already dedispersed (dmc = 1)
+    archive.register_archive("bench_pa_guess", dict(subints=w.model[None, None], freqs=w.freqs,
+                                                    Ps=[w.P], epochs=[(57000, 0, 0.0)],
+                                                    DM=w.DM0, dmc=1))
+    ppalign.align_archives(names[:min(64, narch)], "bench_pa_guess", niter=1, quiet=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    port = ppalign.align_archives(names, "bench_pa_guess", fit_dm=True, niter=niter, quiet=True)
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+    for nm in names + ["bench_pa_guess"]:
+        archive.unregister_archive(nm)
+    del data
+    return {"value": round(narch * niter / t, 1), "unit": "archive-iterations/s",
+            "s_per_call": round(t, 3), "narch": narch, "niter": niter,
+            "ms_per_iteration": round(t / niter * 1e3, 2),
+            "data_gb": round(narch * nchan * nbin * 8 / 1e9, 2),
+            "template_finite": bool(np.isfinite(port).all()),
+            "workload": "config 5: %d archives x 1 subint x %d chan x %d bin, fit_dm, niter %d; "
+                        "setup (registration, unit stack) inside the timed call"
+                        % (narch, nchan, nbin, niter)}
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline: the oracle on the host cores
+# ---------------------------------------------------------------------------
+def cpu_baseline(args, config, data, w, flags, log10_tau, tau_g, host, S):
+    from oracle import cpu_baseline as CB
+    from threadpoolctl import threadpool_limits
+    _, nchan, nbin, _, tau, _, gm, _ = CONFIGS[config]
+    dh = data[:S].cpu().numpy()
+    refs = []
+    ag = w.alpha if flags[3] else 0.0
+    with threadpool_limits(limits=1):  # one core: pin BLAS/OpenMP pools
+        t0 = time.perf_counter()
+        for i in range(S):
+            refs.append(CB.fit_subint(dh[i], w, flags, log10_tau, tau_g, ag))
+        tcpu = time.perf_counter() - t0
+    single = {"value": round(S / tcpu, 3), "unit": "TOAs/s", "cores": 1,
+              "sample": "%d of the bench's own subints in %.1f s" % (S, tcpu)}
+    cores, aff, quota = host_cores()
+    procs = args.cpu_procs or cores
+    per = max(1, int(math.ceil(args.cpu_seconds * S / tcpu)))
+    rate, n_all, t_all = CB.all_cores(procs, per, nchan, nbin, args.seed, tau, gm, flags,
+                                      log10_tau, tau_g, ag, first_sub=S)
+    ratio = timing_ratio(config)
+    cpu = {"value": round(rate, 3), "unit": "TOAs/s", "cores": procs, "kind": "port",
+           "sample": "%d subints of this workload (%s, get_TOAs guess + fit + post-fit incl. "
+                     "noise estimate): %d single-threaded processes x %d subints (>= %.0f s of "
+                     "work each), %.1f s wall; numpy/scipy oracle"
+                     % (n_all, config, procs, per, args.cpu_seconds, t_all),
+           "host_cores": {"affinity": aff, "cgroup_quota": quota, "used": procs},
+           "single_core": single,
+           "oracle_over_reference_time": None if ratio is None else round(ratio, 3),
+           "oracle_over_reference_source": "tests/golden/timing_r3.json (build container, "
+                                           "same subints, 1 thread, config %s)"
+                                           % TIMING_KEY[config],
+           "reference_equivalent_value": None if ratio is None else round(rate * ratio, 3)}
+
+    def gap(i, j):
+        e = refs[i].param_errs[j]
+        return abs(host["params"][i, j] - refs[i].params[j]) / e if e > 0 else 0.0
+    fitted = [j for j in range(5) if flags[j]]
+    parity = {"sample": S, "tolerance": "1e-3 sigma (north_star)",
+              "status_match": bool(all(host["status"][i] == refs[i].return_code
+                                       for i in range(S))),
+              "max_over_sigma": {["phi", "DM", "GM", "tau", "alpha"][j]:
+                                 float(max(gap(i, j) for i in range(S))) for j in fitted}}
+    return cpu, parity
 
 
 def main():
@@ -95,50 +290,40 @@ def main():
         torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
-    from pulseportraiture_amd import synth, pplib
     from pulseportraiture_amd.engine import Engine
-    nsub0, nchan, nbin, flags, tau, log10_tau, gm, desc = CONFIGS[args.config]
+    import pulseportraiture_amd.engine as E
+    config = args.config
+    nsub0, nchan, nbin, flags, tau, log10_tau, gm, desc = CONFIGS[config]
     nsub = args.nsub or nsub0
+    fit_config = "headline" if config == "get_toas" else config
     if args.cpu_sample is None:
-        args.cpu_sample = {"headline": 150, "gm": 40, "scattering": 3}[args.config]
+        args.cpu_sample = {"headline": 150, "gm": 60, "scattering": 4, "get_toas": 0,
+                           "ppalign": 0}[config]
     eng = Engine(local if world > 1 else 0)
-    dev = eng.device
+    E._engines[eng.device.index] = eng  # the drivers' get_engine() uses this context
+
+    if config == "ppalign":
+        return main_ppalign(args, eng, rank, world)
 
     # ---- synthetic inputs, resident in HBM before timing ----
-    w = synth.make_workload(nsub, nchan, nbin, seed=args.seed, sub0=rank * nsub, tau=tau,
-                            gm=gm)
-    data = eng.synth(w.template, w.phase, w.sigma, w.seed, sub0=w.sub0)
-    model = torch.as_tensor(w.model, device=dev)
-    freqs = torch.as_tensor(w.freqs, device=dev)
-    P = torch.full((nsub,), w.P, dtype=torch.float64, device=dev)
-    nu_fit = pplib.guess_fit_freq(w.freqs)  # SNR weights = 1
-    nu = torch.full((nsub, 3), nu_fit, dtype=torch.float64, device=dev)
-    tau_g = 0.0
-    init_row = [0.0, w.DM0, 0.0, 0.0, 0.0]
-    if flags[3]:
-        # pptoas scattering guess: tau at nu_fit from the injected reference value
-        tau_g = tau * (nu_fit / w.nu_ref) ** w.alpha
-        init_row[3] = np.log10(tau_g) if log10_tau else tau_g
-        init_row[4] = w.alpha
-    init = torch.tensor([init_row] * nsub, dtype=torch.float64, device=dev)
-    gtau = torch.full((nsub,), tau_g, dtype=torch.float64, device=dev) if flags[3] else None
+    w, data, kw, tau_g = synth_inputs(eng, fit_config, nsub, args.seed, rank * nsub)
     torch.cuda.synchronize()
-
     small = ["params", "param_errs", "nu_out", "red_chi2", "snr", "status", "nfev"]
-
-    # per-TOA results come back to pinned host buffers, all copies queued on
-    # the stream behind the fit and waited for once (the step's end)
     pinned = {}
 
     def step():
-        out = eng.fit_batch(data, model, freqs, P, init, flags, nu_fit=nu, log10_tau=log10_tau,
-                            guess=True, guess_Ns=100, guess_tau=gtau)
+        out = eng.fit_batch(data, kw["model"], kw["freqs"], kw["P"], kw["init"], flags,
+                            nu_fit=kw["nu"], log10_tau=log10_tau, guess=True, guess_Ns=100,
+                            guess_tau=kw["gtau"])
         for k in small:
             if k not in pinned:
                 pinned[k] = torch.empty(out[k].shape, dtype=out[k].dtype, pin_memory=True)
             pinned[k].copy_(out[k], non_blocking=True)
         torch.cuda.current_stream().synchronize()
         return out, pinned
+
+    if config == "get_toas":
+        return main_get_toas(args, eng, rank, world, w, data, step, desc)
 
     for _ in range(args.warmup):
         out, host = step()
@@ -158,7 +343,7 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=eng.device)
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(tt.item())
     ms_step = elapsed / args.steps * 1e3
@@ -168,28 +353,24 @@ def main():
     ktimes = {}
     if not args.no_timing:
         for name in ["data_xspec", "guess", "moments", "fit_taylor", "solve", "post", "model_fft"]:
-            ms, n = eng.kernel_time(name)
-            ktimes[name] = (ms, n)
+            ktimes[name] = eng.kernel_time(name)
         eng.set_timing(False)
-    status = host["status"].numpy()
-    nfev = host["nfev"].numpy()
+    host = {k: v.numpy().copy() for k, v in host.items()}
+    status, nfev = host["status"], host["nfev"]
 
-    # ---- PCIe-inclusive rate: the same subints from pinned host memory,
-    # copies overlapped with the fits (Engine.fit_batch_streamed); reported
-    # beside value, never as value ----
+    # ---- PCIe-inclusive rate (config gm): the same subints from pinned host
+    # memory, copies overlapped with the fits; reported beside value ----
     hs = args.host_stream if args.host_stream is not None else (
-        max(1, nsub // 8) if args.config == "gm" else 0)
+        max(1, nsub // 8) if config == "gm" else 0)
     stream = None
     if hs and rank == 0:
-        if not args.no_timing:
-            eng.set_timing(False)
-        pinned = torch.empty(tuple(data.shape), dtype=torch.float64, pin_memory=True)
-        pinned.copy_(data)
+        pin = torch.empty(tuple(data.shape), dtype=torch.float64, pin_memory=True)
+        pin.copy_(data)
 
         def sstep():
-            o = eng.fit_batch_streamed(pinned, model, freqs, P, init, flags, chunk=hs, nu_fit=nu,
-                                       log10_tau=log10_tau, guess=True, guess_Ns=100,
-                                       guess_tau=gtau)
+            o = eng.fit_batch_streamed(pin, kw["model"], kw["freqs"], kw["P"], kw["init"], flags,
+                                       chunk=hs, nu_fit=kw["nu"], log10_tau=log10_tau,
+                                       guess=True, guess_Ns=100, guess_tau=kw["gtau"])
             return {k: o[k].to("cpu") for k in small}
         sstep()
         torch.cuda.synchronize()
@@ -202,153 +383,186 @@ def main():
                   "input_gb": round(data.numel() * 8 / 1e9, 3),
                   "pcie_gbs": round(data.numel() * 8 / ts / 1e9, 1),
                   "same_results": bool(all(np.array_equal(np.nan_to_num(hs_host[k].numpy()),
-                                                          np.nan_to_num(host[k].numpy()))
+                                                          np.nan_to_num(host[k]))
                                            for k in small)),
                   "note": "host-resident pinned input, H2D on a second stream overlapped with "
                           "the fits (double buffer); not `value`"}
-        del pinned
+        del pin
+
+    legs = None
+    if rank == 0 and world == 1 and config == "headline" and not args.no_legs:
+        legs = {}
+        g, gt = leg_get_toas(eng, w, data)
+        g["max_dphi_over_sigma_vs_fit_batch"] = float(np.max(
+            np.abs(np.asarray(gt.phis[0]) - host["params"][:, 0]) / host["param_errs"][:, 0]))
+        legs["get_toas"] = g
+        legs["get_toas_host"], _ = leg_get_toas(eng, w, data, reps=1, host=True)
+        legs["ppalign"] = leg_ppalign(eng, args.ppalign_narch, args.ppalign_niter, args.seed)
 
     if rank != 0:
         if world > 1:
             torch.distributed.destroy_process_group()
         return
 
-    # ---- roofline of the dominant kernel (HBM-bound passes over X) ----
-    NHP = ((nbin // 2 + 1) + 7) // 8 * 8
-    nharm = nbin // 2 + 1
-    roof = None
-    if ktimes:
-        dom = max(ktimes, key=lambda k: ktimes[k][0])
-        ms, n = ktimes[dom]
-        avg_s = ms / 1e3 / max(n, 1)
-        if dom == "solve":
-            # algorithmic bytes: every objective pass streams the subint's
-            # cross-spectrum once, 16 B per cell; passes = nfev.
-            # The split scattering solve is a chain of k_scat_sweep /
-            # k_scat_step launches per step: rate over the solve's time per step
-            bytes_launch = float(np.sum(nfev)) * nchan * nharm * 16.0
-            avg_s = ms / 1e3 / args.steps
-            what = ("solve (k_scat_sweep + k_scat_step chain, per step): nfev passes x nchan x "
-                    "nharm x 16 B of X per subint")
-        elif dom == "data_xspec":
-            bytes_launch = nsub * (8.0 * nchan * nbin + 16.0 * nchan * nharm)
-            what = "k_data_xspec: 8 B/sample read + 16 B/cell X written"
-        elif dom == "moments":
-            bytes_launch = nsub * 16.0 * nchan * nharm
-            what = "k_moments: 16 B/cell X read once (32 Taylor moments per channel written)"
-        elif dom == "post":
-            bytes_launch = nsub * nchan * nharm * 16.0
-            what = "k_post: one with-scales pass over X"
-        else:
-            bytes_launch = nsub * nharm * 16.0 * 2
-            what = "k_guess: R and mean-template spectra"
-        lps = max(n / args.steps, 1.0) if dom != "solve" else 1.0
-        bytes_launch /= lps  # the chunk may run as several pieces (ppf_set_pipeline)
-        achieved = bytes_launch / avg_s / 1e9
-        traffic = pmc_traffic(dom, nsub, nbin, nchan, args.config)
-        if traffic:
-            traffic /= lps
-        roof = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic, "traffic_unit": "bytes/launch",
-                "traffic_source": os.path.relpath(PMC_TRAFFIC, ROOT) if traffic else None,
-                "avg_launch_ms": round(avg_s * 1e3, 4),
-                "algorithmic_bytes_per_launch": bytes_launch, "bytes_model": what,
-                "kernel_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in ktimes.items()},
-                "kernel_launches_per_step": {k: round(v[1] / args.steps, 2) for k, v in ktimes.items()}}
+    roof, others = roofline(args, config, nsub, nchan, nbin, flags, tau, ktimes, nfev)
 
-    # ---- the next-largest kernels against their own bounds (only kernels
-    # that did this config's work: each subint runs in exactly one solver
-    # variant, the others exit at once) ----
-    others = {}
-    taylor = not flags[3] and tau == 0.0
-    if ktimes:
-        def avg_ms(k):  # per step's worth of subints (all pieces of the chunk)
-            ms, n = ktimes[k]
-            return ms / max(n, 1) * max(n / args.steps, 1.0)
-        if taylor and ktimes.get("moments", (0, 0))[1]:
-            t = avg_ms("moments") / 1e3
-            # T = V (32 x nharm powers v^m) . W (nharm x 2 nchan), fp64 MFMA
-            fl = nsub * 2.0 * 32 * nharm * 2 * nchan
-            tf = fl / t / 1e12
-            if tf <= FP64_PEAK_TFLOPS:
-                others["moments"] = {"bound": "mfma-f64", "achieved_tflops": round(tf, 2),
-                                     "peak_tflops": FP64_PEAK_TFLOPS,
-                                     "frac": round(tf / FP64_PEAK_TFLOPS, 4),
-                                     "hbm_gbs": round(nsub * 16.0 * nchan * nharm / t / 1e9, 1),
-                                     "avg_launch_ms": round(avg_ms("moments"), 4)}
-        if ktimes.get("data_xspec", (0, 0))[1] and roof and roof["kernel"] != "data_xspec":
-            t = avg_ms("data_xspec") / 1e3
-            b = nsub * (8.0 * nchan * nbin + 16.0 * nchan * nharm)
-            others["data_xspec"] = {"bound": "hbm", "achieved_gbs": round(b / t / 1e9, 1),
-                                    "frac": round(b / t / 1e9 / HBM_PEAK_GBS, 4)}
-    if roof is not None:
-        roof["other_kernels"] = others
-        if roof["frac"] > 1.0:  # the timed kernel cannot have done this work
-            roof["frac"] = roof["achieved"] = None
-            roof["bytes_model"] += " (INVALID: above peak)"
-
-    # ---- CPU baseline: the oracle's get_TOAs step on host cores ----
-    cpu = None
-    parity = None
-    S = min(args.cpu_sample, nsub) if args.cpu_sample > 0 else 0
+    # ---- CPU baseline: the oracle's get_TOAs step on the host cores ----
+    cpu = parity = None
+    S = min(args.cpu_sample, nsub) if args.cpu_sample > 0 and world == 1 else 0
     if S:
-        from oracle import cpu_baseline as CB
-        from threadpoolctl import threadpool_limits
-        dh = data[:S].cpu().numpy()
-        refs = []
-        ag = w.alpha if flags[3] else 0.0
-        with threadpool_limits(limits=1):  # one core: pin BLAS/OpenMP pools
-            t0 = time.perf_counter()
-            for i in range(S):
-                refs.append(CB.fit_subint(dh[i], w, flags, log10_tau, tau_g, ag))
-            tcpu = time.perf_counter() - t0
-        single = {"value": round(S / tcpu, 3), "unit": "TOAs/s", "cores": 1,
-                  "sample": "%d of the bench's own subints in %.1f s" % (S, tcpu)}
-        procs = min(args.cpu_procs, os.cpu_count() or 1)
-        per = max(1, int(round(args.cpu_seconds * S / tcpu / procs)))
-        rate, n_all, t_all = CB.all_cores(procs, per, nchan, nbin, args.seed, tau, gm, flags,
-                                          log10_tau, tau_g, ag, first_sub=S)
-        ratio_file = os.path.join(ROOT, "tests", "golden", "timing_r2.json")
-        ref_ratio = json.load(open(ratio_file)) if os.path.exists(ratio_file) else None
-        cpu = {"value": round(rate, 3), "unit": "TOAs/s", "cores": procs, "kind": "port",
-               "sample": "%d subints of this workload (%s, get_TOAs guess + fit + post-fit "
-                         "incl. noise estimate), %d single-threaded processes x %d subints, "
-                         "%.1f s wall; numpy/scipy oracle" % (n_all, args.config, procs, per,
-                                                              t_all),
-               "single_core": single,
-               "oracle_over_reference_time": None if ref_ratio is None else
-               round(ref_ratio["ratio_oracle_over_reference"], 3),
-               "oracle_over_reference_source": "tests/golden/timing_r2.json (build container, "
-                                               "64x2048 phase+DM, 1 thread)"}
-        def gap(i, j):
-            e = refs[i].param_errs[j]
-            return abs(host["params"].numpy()[i, j] - refs[i].params[j]) / e if e > 0 else 0.0
-        fitted = [j for j in range(5) if flags[j]]
-        parity = {"sample": S, "tolerance": "1e-3 sigma (north_star)",
-                  "status_match": bool(all(status[i] == refs[i].return_code for i in range(S))),
-                  "max_over_sigma": {["phi", "DM", "GM", "tau", "alpha"][j]:
-                                     float(max(gap(i, j) for i in range(S))) for j in fitted}}
+        cpu, parity = cpu_baseline(args, config, data, w, flags, log10_tau, tau_g, host, S)
 
     line = {
         "metric": "TOAs/sec (phase+DM fit, 64ch×2048bin fp64) at 1/2/4/8 MI355X"
-        if args.config == "headline" else "TOAs/sec (%s)" % args.config,
+        if config == "headline" else "TOAs/sec (%s)" % config,
         "value": round(value, 2), "unit": "TOAs/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (example.gmodel template, injected phi/DM, sigma=1.5 Philox "
                 "noise; generated on device)",
         "config": {"workload": desc, "nsub_per_gpu": nsub, "nchan": nchan, "nbin": nbin,
-                   "fit_flags": flags, "guess_Ns": 100, "parallelism": "subint-sharded dp%d" % world},
+                   "fit_flags": flags, "guess_Ns": 100,
+                   "parallelism": "subint-sharded dp%d" % world},
         "status_counts": {str(k): int(v) for k, v in zip(*np.unique(status, return_counts=True))},
         "mean_nfev": float(np.mean(nfev)),
         "roofline": roof, "cpu_baseline": cpu, "parity_sample": parity,
-        "host_stream": stream,
+        "host_stream": stream, "legs": legs,
         "gpu_over_cpu": None if not cpu else round(value / cpu["value"], 1),
     }
     print(json.dumps(line))
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+def roofline(args, config, nsub, nchan, nbin, flags, tau, ktimes, nfev):
+    """Dominant kernel against its bound: HBM for the streaming passes, the
+    fp64 VALU peak for the scattering sweeps (config 3)."""
+    nharm = nbin // 2 + 1
+    if not ktimes:
+        return None, None
+    dom = max(ktimes, key=lambda k: ktimes[k][0])
+    ms, n = ktimes[dom]
+    avg_s = ms / 1e3 / max(n, 1)
+    lps = max(n / args.steps, 1.0)
+    if dom == "solve":
+        # the split scattering solve is a chain of k_scat_sweep / k_scat_step
+        # launches per step: every objective pass evaluates nchan x nharm cells
+        cells = float(np.sum(nfev)) * nchan * nharm
+        t = ms / 1e3 / args.steps
+        flops = cells * SCAT_FLOPS_PER_CELL
+        tf = flops / t / 1e12
+        roof = {"kernel": "solve (k_scat_sweep + k_scat_step chain, per step)", "bound": "fp64",
+                "achieved": round(tf, 2), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(tf / FP64_PEAK_TFLOPS, 4), "traffic": pmc_traffic(dom, nsub, config),
+                "traffic_unit": "bytes per step (k_scat_sweep launches)",
+                "avg_launch_ms": round(t * 1e3, 4), "algorithmic_flops_per_launch": flops,
+                "flops_model": "sum(nfev) x nchan x nharm cell evaluations x %.0f fp64 flops "
+                               "(cells_scat)" % SCAT_FLOPS_PER_CELL,
+                "hbm_gbs": round(cells * 24.0 / t / 1e9, 1)}
+    else:
+        if dom == "data_xspec":
+            b = nsub * (8.0 * nchan * nbin + 16.0 * nchan * nharm)
+            what = "k_data_xspec: 8 B/sample read + 16 B/cell X written"
+        elif dom == "moments":
+            b = nsub * 16.0 * nchan * nharm
+            what = "k_moments: 16 B/cell X read once (32 Taylor moments per channel written)"
+        elif dom == "post":
+            b = nsub * nchan * nharm * 16.0
+            what = "k_post: one with-scales pass over X"
+        else:
+            b = nsub * nharm * 16.0 * 2
+            what = "k_guess: R and mean-template spectra"
+        b /= lps  # the chunk may run as several pieces (ppf_set_pipeline)
+        achieved = b / avg_s / 1e9
+        traffic = pmc_traffic(dom, nsub, config)
+        if traffic:
+            traffic /= lps
+        roof = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic, "traffic_unit": "bytes/launch",
+                "avg_launch_ms": round(avg_s * 1e3, 4), "algorithmic_bytes_per_launch": b,
+                "bytes_model": what}
+    src = PMC_TRAFFIC.get(config)
+    roof["traffic_source"] = os.path.relpath(src, ROOT) if (src and roof["traffic"]) else None
+    roof["kernel_ms_per_step"] = {k: round(v[0] / args.steps, 4) for k, v in ktimes.items()}
+    roof["kernel_launches_per_step"] = {k: round(v[1] / args.steps, 2) for k, v in ktimes.items()}
+    others = {}
+    taylor = not flags[3] and tau == 0.0
+
+    def avg_ms(k):  # per step's worth of subints (all pieces of the chunk)
+        m, c = ktimes[k]
+        return m / max(c, 1) * max(c / args.steps, 1.0)
+    if taylor and ktimes.get("moments", (0, 0))[1]:
+        t = avg_ms("moments") / 1e3
+        # T = V (32 x nharm powers v^m) . W (nharm x 2 nchan), fp64 MFMA
+        fl = nsub * 2.0 * 32 * nharm * 2 * nchan
+        tf = fl / t / 1e12
+        others["moments"] = {"bound": "mfma-f64", "achieved_tflops": round(tf, 2),
+                             "peak_tflops": FP64_PEAK_TFLOPS,
+                             "frac": round(tf / FP64_PEAK_TFLOPS, 4),
+                             "hbm_gbs": round(nsub * 16.0 * nchan * nharm / t / 1e9, 1),
+                             "hbm_frac": round(nsub * 16.0 * nchan * nharm / t / 1e9 /
+                                               HBM_PEAK_GBS, 4),
+                             "avg_launch_ms": round(avg_ms("moments"), 4)}
+    if ktimes.get("data_xspec", (0, 0))[1] and roof["kernel"] != "data_xspec":
+        t = avg_ms("data_xspec") / 1e3
+        b = nsub * (8.0 * nchan * nbin + 16.0 * nchan * nharm)
+        others["data_xspec"] = {"bound": "hbm", "achieved_gbs": round(b / t / 1e9, 1),
+                                "frac": round(b / t / 1e9 / HBM_PEAK_GBS, 4),
+                                "avg_launch_ms": round(t * 1e3, 4)}
+    roof["other_kernels"] = others
+    if roof["frac"] is not None and roof["frac"] > 1.0:  # the timed kernel cannot have done it
+        roof["frac"] = roof["achieved"] = None
+        roof["invalid"] = "above peak"
+    return roof, others
+
+
+def main_get_toas(args, eng, rank, world, w, data, step, desc):
+    """--config get_toas: value = GetTOAs.get_TOAs TOAs/s on a registered
+    archive of the bench's subints (device-resident), .tim text included."""
+    import torch
+    if world > 1:
+        raise SystemExit("--config get_toas runs on one GPU (get_TOAs shards itself when "
+                         "torch.distributed is initialised; see tests)")
+    steps = max(1, args.steps)
+    g, gt = leg_get_toas(eng, w, data, reps=steps)
+    out, host = step()
+    host = {k: v.numpy().copy() for k, v in host.items()}
+    same = float(np.max(np.abs(np.asarray(gt.phis[0]) - host["params"][:, 0]) /
+                        host["param_errs"][:, 0]))
+    gh, _ = leg_get_toas(eng, w, data, reps=1, host=True)
+    nsub = data.shape[0]
+    line = {"metric": "TOAs/sec (GetTOAs.get_TOAs end to end, 64ch×2048bin phase+DM fp64)",
+            "value": g["value"], "unit": "TOAs/s", "n_gpus": 1, "steps": steps, "warmup": 1,
+            "ms_per_step": g["ms_per_call"], "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (example.gmodel template, injected phi/DM, sigma=1.5 Philox "
+                    "noise; generated on device)",
+            "config": {"workload": desc, "nsub_per_gpu": nsub, "nchan": 64, "nbin": 2048,
+                       "fit_flags": [1, 1, 0, 0, 0], "guess_Ns": 100, "parallelism": "dp1"},
+            "tim_lines": g["tim_lines"], "max_dphi_over_sigma_vs_fit_batch": same,
+            "host_resident": gh, "roofline": None, "cpu_baseline": None}
+    print(json.dumps(line))
+
+
+def main_ppalign(args, eng, rank, world):
+    """--config ppalign: value = archive-iterations/s of align_archives at
+    config 5 (4096 x 256 x 2048, niter 3)."""
+    if world > 1:
+        raise SystemExit("--config ppalign runs on one GPU here; align_archives shards its "
+                         "units and all-reduces when torch.distributed is initialised")
+    narch = args.nsub or args.ppalign_narch
+    r = leg_ppalign(eng, narch, args.ppalign_niter, args.seed)
+    line = {"metric": "archive-iterations/sec (ppalign.align_archives, 256ch×2048bin fp64)",
+            "value": r["value"], "unit": r["unit"], "n_gpus": 1, "steps": 1, "warmup": 1,
+            "ms_per_step": round(r["s_per_call"] * 1e3, 2), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (example.gmodel template, injected phi/DM, sigma=1.5 Philox "
+                    "noise; generated on device)",
+            "config": {"workload": r["workload"], "narch": narch, "nchan": 256, "nbin": 2048,
+                       "niter": args.ppalign_niter, "parallelism": "dp1"},
+            "detail": r, "roofline": None, "cpu_baseline": None}
+    print(json.dumps(line))
 
 
 if __name__ == "__main__":

@@ -98,6 +98,11 @@ int ppf_set_pipeline(ppf_ctx* ctx, int32_t pieces);
 int ppf_set_workspace_limit(ppf_ctx* ctx, int64_t bytes);
 /* Per-kernel HIP-event timing on the context stream (off by default). */
 int ppf_set_timing(ppf_ctx* ctx, int enable);
+/* Diagnostic: record every objective sweep of the TNC and Newton-CG solvers
+ * (the point, f, gradient, Hessian terms, whether it counts in nfev) into
+ * buf [nsub][cap][32] doubles (device memory, caller-owned; batch subint
+ * index), at most cap sweeps per subint.  cap 0 turns it off.             */
+int ppf_set_trace(ppf_ctx* ctx, double* buf, int32_t cap);
 int ppf_get_kernel_time(ppf_ctx* ctx, int kernel_id, double* total_ms,
                         int64_t* launches);
 int ppf_reset_kernel_times(ppf_ctx* ctx);

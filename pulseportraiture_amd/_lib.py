@@ -65,6 +65,7 @@ EXPORTS = {
     "ppf_set_pipeline": ([ctypes.c_void_p, ctypes.c_int32], ctypes.c_int),
     "ppf_set_workspace_limit": ([ctypes.c_void_p, ctypes.c_int64], ctypes.c_int),
     "ppf_set_timing": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
+    "ppf_set_trace": ([ctypes.c_void_p, _dp, ctypes.c_int32], ctypes.c_int),
     "ppf_get_kernel_time": ([ctypes.c_void_p, ctypes.c_int,
                              ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(ctypes.c_int64)], ctypes.c_int),

@@ -52,6 +52,8 @@ struct ppf_ctx {
   bool timing = false;
   std::vector<TimedLaunch> pending;
   std::vector<hipEvent_t> pool;
+  double* trace = nullptr;  // solver trace buffer (ppf_set_trace), device
+  int trace_cap = 0;
   double ktime[PPF_NUM_KERNELS] = {0};
   int64_t klaunch[PPF_NUM_KERNELS] = {0};
 };
@@ -331,6 +333,13 @@ int ppf_set_workspace_limit(ppf_ctx* ctx, int64_t bytes) {
   return PPF_OK;
 }
 
+int ppf_set_trace(ppf_ctx* ctx, double* buf, int32_t cap) {
+  if (!ctx || cap < 0 || (cap > 0 && !buf)) return PPF_ERR_INVALID;
+  ctx->trace = buf;
+  ctx->trace_cap = cap;
+  return PPF_OK;
+}
+
 int ppf_set_timing(ppf_ctx* ctx, int enable) {
   if (!ctx) return PPF_ERR_INVALID;
   ctx->timing = enable != 0;
@@ -499,6 +508,8 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
     if (int r = vpow_table(ctx, nbin, &fa.vpow)) return r;
   fa.Mmean = Mmean;
   fa.ptime = ctx->phase_prof ? static_cast<unsigned long long*>(ctx->ptime.p) : nullptr;
+  fa.trace = ctx->trace_cap > 0 ? ctx->trace : nullptr;
+  fa.trace_cap = ctx->trace_cap;
   fa.o_params = o->params;
   fa.o_param_errs = o->param_errs;
   fa.o_nu_out = o->nu_out;

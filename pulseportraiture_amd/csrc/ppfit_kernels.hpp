@@ -104,6 +104,8 @@ struct FitArgs {
   const double2* vpow;       // [kVpowRows(N)][16] (v^col, v^(16+col)), v = k / N
   const double2* Mmean;      // [nmodel][NHP] mean template spectrum or null
   unsigned long long* ptime; // [PPF_PHASE_N] k_fit_taylor phase clocks, or null
+  double* trace;             // solver trace (ppf_set_trace): [nsub][trace_cap][kTraceRec]
+  int trace_cap;             //   objective sweeps recorded per subint (0: off)
   double* acc;               // chunk [c][2][nchan][10]
   double* wsc;               // chunk [c][nchan][8]
   // outputs (global batch index sub0 + c)
@@ -126,6 +128,20 @@ struct FitArgs {
   double* o_hess;            // [nsub][25] or null
   double bounds[5][2];       // TNC bounds (NaN = None)
 };
+
+// One solver-trace record (diagnostic, ppf_set_trace): the point, f, the
+// masked gradient and the 15 Hessian terms of one objective sweep, whether
+// scipy counts it in nfev, and the sweep's index.  Written by thread 0.
+constexpr int kTraceRec = 32;
+__device__ __forceinline__ void trace_sweep(const FitArgs& a, int s, int isweep, const double* x,
+                                            const double* out, int nout, bool counted) {
+  if (!a.trace || threadIdx.x != 0 || isweep >= a.trace_cap) return;
+  double* r = a.trace + ((size_t)s * a.trace_cap + isweep) * kTraceRec;
+  for (int i = 0; i < 5; ++i) r[i] = x[i];
+  for (int i = 0; i < 21; ++i) r[5 + i] = i < nout ? out[i] : NAN;
+  r[26] = counted ? 1.0 : 0.0;
+  r[27] = (double)isweep;
+}
 
 // ---------------------------------------------------------------------------
 // FFTFIT search on a staged cross-spectrum rm_k = R_k conj(M_k), k < NH:

@@ -38,6 +38,7 @@ struct Obj {
   double lx[N], lf, lg[N], lH[N][N];
   bool have;
   int nfev;
+  int nsweep;  // sweeps so far (the trace index)
   // f, g, H at x (a sweep unless x is the cached point); count: scipy
   // evaluates f there (nfev)
   template <bool SCAT>
@@ -51,6 +52,7 @@ struct Obj {
 #pragma unroll
     for (int i = 0; i < N; ++i) pr[i] = x[i];
     sweep<0, SCAT>(*a, *m, c, s, pr, refs, P, acc_slot, out, red, TaylorSrc{});
+    trace_sweep(*a, s, nsweep++, pr, out, 21, count);
     lf = out[0];
 #pragma unroll
     for (int i = 0; i < N; ++i) {
@@ -560,6 +562,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_ncg(FitArgs a) {
   O.out = sh.out;
   O.have = false;
   O.nfev = 0;
+  O.nsweep = 0;
   int status = -1;
   double f = NAN;
   if (m.nok > 0) {

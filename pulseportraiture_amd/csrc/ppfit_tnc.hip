@@ -325,6 +325,7 @@ struct TncObjective {
 #pragma unroll
       for (int i = 0; i < 5; ++i) pr[i] = i < n ? x[i] : lastx[i];
       sweep<0, SCAT>(*a, *m, c, s, pr, refs, P, acc_slot, out, red, TaylorSrc{});
+      trace_sweep(*a, s, nfev, pr, out, 6, true);
       lastf = out[0];
 #pragma unroll
       for (int i = 0; i < 5; ++i) {
@@ -920,6 +921,9 @@ __global__ __launch_bounds__(kBlock, 1) void k_tnc(FitArgs a) {
       const double dof = (double)a.nbin * (double)m.nok - (double)(nfit + m.nok);
       fmin = dof - sd;
     }
+    // the trace's record 0 carries the minfev TNC was given (field 29)
+    if (a.trace && tid == 0 && a.trace_cap > 0)
+      a.trace[(size_t)s * a.trace_cap * kTraceRec + 29] = fmin;
     TncState T;
     T.n = n;
     T.maxfun = 100;  // max(100, 10 n), n <= 5

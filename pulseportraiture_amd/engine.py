@@ -117,6 +117,16 @@ class Engine:
     def set_timing(self, on=True):
         self._chk(self.lib.ppf_set_timing(self.ctx, int(bool(on))))
 
+    def set_trace(self, buf, cap):
+        """Solver trace of the TNC / Newton-CG kernels (ppf_set_trace): buf a
+        float64 device tensor [nsub, cap, 32] or None (off)."""
+        if buf is None or cap <= 0:
+            self._chk(self.lib.ppf_set_trace(self.ctx, None, 0))
+            self._trace = None
+            return
+        self._trace = buf
+        self._chk(self.lib.ppf_set_trace(self.ctx, _ptr(buf), int(cap)))
+
     def kernel_time(self, name):
         ms = ctypes.c_double()
         n = ctypes.c_int64()
@@ -265,33 +275,52 @@ class Engine:
             np.ascontiguousarray(host_data, dtype=np.float64))
         nsub, nchan, nbin = hd.shape
         chunk = max(1, min(int(chunk), nsub))
+        # pageable input: each chunk is staged into one of two pinned buffers
+        # on the host (a CPU copy that overlaps the previous chunk's fit),
+        # then copied to the device asynchronously
+        staged = not hd.is_pinned()
+        pin = [torch.empty((chunk, nchan, nbin), dtype=torch.float64, pin_memory=True)
+               for _ in range(2)] if staged else None
 
-        def part(v, s0, s1):
-            if v is None or np.ndim(v) == 0:
-                return v
-            if isinstance(v, (list, tuple)) and not len(v):
+        # per-subint arguments and the ndim at which they carry a subint axis
+        # (a [nchan] freqs row or a [5] init row is shared, never sliced)
+        per_sub = {"freqs": 2, "P": 1, "init": 2, "nu_fit": 2, "nu_out": 2, "errs": 2,
+                   "chan_mask": 2, "weights": 2, "model_idx": 1, "guess_nu": 1, "guess_tau": 1}
+
+        def part(name, v, s0, s1):
+            if v is None or isinstance(v, (int, float)):
                 return v
             a = v if isinstance(v, torch.Tensor) else np.asarray(v)
-            return a[s0:s1] if a.shape[0] == nsub and nsub > 1 else a
+            if a.ndim == per_sub[name] and a.shape[0] == nsub:
+                return a[s0:s1]
+            return a
 
-        per_sub = ["nu_fit", "nu_out", "errs", "chan_mask", "weights", "model_idx", "guess_nu",
-                   "guess_tau"]
         comp = self.stream
         copy = torch.cuda.Stream(dev)
         bufs = [torch.empty((chunk, nchan, nbin), dtype=torch.float64, device=dev)
                 for _ in range(2)]
         copied = [torch.cuda.Event() for _ in range(2)]
         free = [torch.cuda.Event() for _ in range(2)]
+        h2d_done = [None, None]
         nchunks = (nsub + chunk - 1) // chunk
 
         def issue(i):
             s0 = i * chunk
             n = min(chunk, nsub - s0)
+            src = hd[s0:s0 + n]
+            if staged:
+                if h2d_done[i % 2] is not None:
+                    h2d_done[i % 2].synchronize()  # the pinned buffer's last H2D finished
+                pin[i % 2][:n].copy_(src)
+                src = pin[i % 2][:n]
             with torch.cuda.stream(copy):
                 if i >= 2:
                     copy.wait_event(free[i % 2])  # chunk i - 2 is done with the buffer
-                bufs[i % 2][:n].copy_(hd[s0:s0 + n], non_blocking=True)
+                bufs[i % 2][:n].copy_(src, non_blocking=True)
                 copied[i % 2].record(copy)
+                if staged:
+                    h2d_done[i % 2] = torch.cuda.Event()
+                    h2d_done[i % 2].record(copy)
 
         outs = []
         issue(0)
@@ -304,9 +333,10 @@ class Engine:
             kwi = dict(kw)
             for k in per_sub:
                 if k in kwi:
-                    kwi[k] = part(kwi[k], s0, s1)
-            r = self.fit_batch(bufs[i % 2][:s1 - s0], model, part(freqs, s0, s1),
-                               part(P, s0, s1), part(init, s0, s1), fit_flags, **kwi)
+                    kwi[k] = part(k, kwi[k], s0, s1)
+            r = self.fit_batch(bufs[i % 2][:s1 - s0], model, part("freqs", freqs, s0, s1),
+                               part("P", P, s0, s1), part("init", init, s0, s1), fit_flags,
+                               **kwi)
             free[i % 2].record(comp)
             outs.append(r)
         return {k: torch.cat([o[k] for o in outs]) for k in outs[0]

@@ -72,6 +72,12 @@ def instrumental_response_FT(nbin, wid=0.0, irf_type="rect"):
     return instrumental_response_port_FT(nbin, [1.0], 0.0, 1.0, [wid], [irf_type])[0]
 
 
+# host inputs above STREAM_BYTES are fitted in chunks of STREAM_CHUNK_BYTES
+# with the host -> device copies overlapped (fit_portraits_batch)
+STREAM_BYTES = 1 << 30
+STREAM_CHUNK_BYTES = 1 << 29
+
+
 def _nan(v):
     return np.nan if v is None else float(v)
 
@@ -90,14 +96,25 @@ def fit_portraits_batch(data, model, init, P, freqs, nu_fits=None, nu_outs=None,
         print("Method '%s' is not implemented." % method)
         sys.exit()
     from .engine import get_engine
+    import torch
     eng = get_engine(device)
     t0 = time.time()
-    out = eng.fit_batch(data, model, freqs, P, init, fit_flags, nu_fit=nu_fits,
-                        nu_out=nu_outs, errs=errs, chan_mask=chan_mask, weights=weights,
-                        model_idx=model_idx, log10_tau=log10_tau, option=option,
-                        is_toa=is_toa, guess=guess, guess_Ns=guess_Ns,
-                        guess_wrap=guess_wrap, guess_nu=guess_nu, guess_tau=guess_tau,
-                        method=method, bounds=bounds if method.startswith("TNC") else None)
+    kw = dict(nu_fit=nu_fits, nu_out=nu_outs, errs=errs, chan_mask=chan_mask, weights=weights,
+              model_idx=model_idx, log10_tau=log10_tau, option=option, is_toa=is_toa,
+              guess=guess, guess_Ns=guess_Ns, guess_wrap=guess_wrap, guess_nu=guess_nu,
+              guess_tau=guess_tau, method=method,
+              bounds=bounds if method.startswith("TNC") else None)
+    host = not isinstance(data, torch.Tensor) or data.device.type == "cpu"
+    nbytes = int(np.prod(np.shape(data))) * 8
+    if host and np.ndim(data) == 3 and nbytes > STREAM_BYTES:
+        # host-resident subints: chunks staged through pinned buffers and
+        # copied to the device on a second stream while the previous chunk is
+        # fitted (Engine.fit_batch_streamed)
+        per = int(np.prod(np.shape(data)[1:])) * 8
+        out = eng.fit_batch_streamed(data, model, freqs, P, init, fit_flags,
+                                     chunk=max(1, STREAM_CHUNK_BYTES // per), **kw)
+    else:
+        out = eng.fit_batch(data, model, freqs, P, init, fit_flags, **kw)
     if not to_host:
         return out
     res = {k: v.cpu().numpy() for k, v in out.items() if not k.startswith("_")}

@@ -1,20 +1,20 @@
 """PSRFITS archives for load_data.
 
-``load_psrfits(path)`` returns the DataBunch that pplib.load_data builds with
-PSRCHIVE (pplib.py:2650-2820) for a fold-mode PSRFITS file: the host reader
-``libppfits.so`` (include/ppfits.h, plain C++) parses the headers and tables
-and returns the raw DATA column; the GPU turns the 8/16-bit samples into
-physical values and sums the polarisations (``ppf_unpack_subints``), and
-the per-channel noise is get_noise_PS on the device, as load_data's
-``noise_stds`` (pplib.py:2740-2748).
+``PSRFITSSource`` is the archive.Archive source for a fold-mode PSRFITS
+file: the host reader ``libppfits.so`` (include/ppfits.h, plain C++) parses
+the headers and tables and returns the raw DATA column of any subint range;
+the GPU turns the 8/16-bit samples into physical values and sums the
+polarisations (``ppf_unpack_subints``).  load_data's processing
+(dedisperse / dededisperse, remove_baseline, tscrunch) then runs on the device
+in archive.py, and the per-channel noise is get_noise_PS on the device, as
+load_data's ``noise_stds`` (pplib.py:2740-2748).
 
 What PSRCHIVE computes from resources this build does not have is set as
 follows, and documented in DESIGN.md: Doppler factors 1 (PSRCHIVE derives
 them from the ephemeris and observatory), channel S/N 1 (Profile.snr()
-weights only guess_fit_freq's reference frequency), no baseline removal
-(get_TOAs loads with rm_baseline=False, pptoas.py:25-29).  The folding
-period is the SUBINT PERIOD column when present, else the POLYCO predictor's
-frequency at the subint epoch.
+weights only guess_fit_freq's reference frequency).  The folding period is
+the SUBINT PERIOD column when present, else the POLYCO predictor's frequency
+at the subint epoch; the DEDISP flag of the last HISTORY row is ``dmc``.
 """
 import ctypes
 import os

@@ -247,3 +247,53 @@ def test_channels_to_zap_vs_reference(gpu):
                                                 return_fit=True, quiet=True)
     rc = [np.sum(((port[c] - model[c]) / noise[c]) ** 2) / (port.shape[1] - 2) for c in ok]
     np.testing.assert_allclose(rc, z["noiter_rchi2_1"], rtol=1e-5)
+
+
+def test_get_toas_config1_example_shape(gpu, tmp_path):
+    """BASELINE config 1 (examples/example.py plumbing): 5 archives x 10
+    subints x 64 x 512, phase+DM, one with a zapped channel in two subints and
+    a fully zapped subint, against the reference's own get_TOAs
+    (tests/golden/make_golden_cfg1.py)."""
+    from pulseportraiture_amd import archive, pplib, pptoas, synth
+    meta = json.load(open(os.path.join(GOLDEN, "config1.json")))
+    z = np.load(os.path.join(GOLDEN, "config1.npz"))
+    c = meta["cfg"]
+    names = meta["archives"]
+    for ia, name in enumerate(names):
+        register_synth_archive(name, c["nsub"], c["nchan"], c["nbin"], c["seed"] + ia, 0.0, 0.0)
+        b = dict(archive._registry[name])
+        w = np.ones((c["nsub"], c["nchan"]))
+        if ia == 2:  # make_golden_cfg1.zap_weights
+            w[3, 9] = w[4, 9] = 0.0
+            w[7] = 0.0
+        b["weights"] = w
+        for k in ("ok_isubs", "ok_ichans", "masks"):
+            b.pop(k)
+        archive.register_archive(name, b)
+    shutil.copy(synth.EXAMPLE_GMODEL, os.path.join(tmp_path, "example.gmodel"))
+    cwd = os.getcwd()
+    os.chdir(tmp_path)
+    try:
+        gt = pptoas.GetTOAs(names, "example.gmodel", quiet=True)
+        gt.get_TOAs(quiet=True)
+        lines = [pplib.toa_line(t) for t in gt.TOA_list]
+    finally:
+        os.chdir(cwd)
+    assert len(lines) == 49
+    worst = 0.0
+    for ia in range(len(names)):
+        p = "a%d_" % ia
+        ok = gt.ok_isubs[ia]
+        assert np.array_equal(ok, z[p + "ok_isubs"])
+        assert np.array_equal(gt.rcs[ia][ok], z[p + "rcs"][ok])
+        for attr, err in [("phis", "phi_errs"), ("DMs", "DM_errs")]:
+            e = z[p + err][ok]
+            d = np.abs(np.asarray(getattr(gt, attr)[ia])[ok] - z[p + attr][ok]) / e
+            worst = max(worst, d.max())
+            assert np.all(d <= 1e-3), (ia, attr, d.max())
+        np.testing.assert_allclose(np.array(gt.nu_fits[ia])[ok], z[p + "nu_fits"][ok],
+                                   rtol=1e-12)
+        dd, de = z[p + "DeltaDM"]
+        assert abs(gt.DeltaDM_means[ia] - dd) <= 1e-3 * de
+    print("config 1: 49 TOAs, max |delta| / sigma %.3g" % worst)
+    compare_tim(lines, meta["tim"])
