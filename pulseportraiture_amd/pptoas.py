@@ -577,8 +577,9 @@ class GetTOAs:
                         m = get_engine().spline_portraits(spline[3], spline[4], spline[5],
                                                           freqs, nbin).cpu().numpy()
                 if irf:
-                    fx = freqs[data.ok_ichans[isub]]
-                    cbw = abs(fx[1] - fx[0]) if len(fx) > 1 else 0.0
+                    # show_fit passes the full freqs row (pptoas.py:1384-1386),
+                    # so chan_bw is |freqs[1] - freqs[0]| over all channels
+                    cbw = abs(freqs[1] - freqs[0]) if len(freqs) > 1 else 0.0
                     from .engine import get_engine
                     m = get_engine().instrumental_response_rows(
                         np.asarray(m, dtype=np.float64), freqs, self.ird["DM"], P,

@@ -150,3 +150,37 @@ def test_align_archives_golden(gpu):
         port = ppalign.align_archives(names, "guess.fits", fit_dm=True, niter=niter, quiet=True)
         ref = z["aligned_niter%d" % niter]
         np.testing.assert_allclose(port, ref, atol=1e-6 * np.abs(ref).max())
+
+
+def test_get_toas_two_channel_fit_flags(gpu, tmp_path):
+    """get_TOAs' fit_flags quirk for 2-channel subints with fit_DM and fit_GM
+    (pptoas.py:474-484): the flags list is carried across subints, so a
+    2-channel subint fits the *previous* subint's flags with GM off, and one
+    with no subint before it raises the reference's UnboundLocalError (kept
+    for parity)."""
+    from pulseportraiture_amd import archive, pptoas, synth
+    w = synth.make_workload(3, 8, 256, seed=31)
+    data = synth.workload_data_host(w)[:, None]
+    wts = np.ones((3, 8))
+    wts[1, 2:] = 0.0  # subint 1: two channels
+    base = dict(subints=data, freqs=w.freqs, Ps=np.full(3, w.P), DM=DM0, nu0=1500.0,
+                epochs=[(57000 + k, 0, 0.0) for k in range(3)], weights=wts)
+    archive.register_archive("twoch_mid", base)
+    w0 = wts.copy()
+    w0[0, 2:] = 0.0  # subint 0: two channels, nothing before it
+    archive.register_archive("twoch_first", dict(base, weights=w0))
+    shutil.copy(synth.EXAMPLE_GMODEL, str(tmp_path / "example.gmodel"))
+    cwd = os.getcwd()
+    os.chdir(tmp_path)
+    try:
+        gt = pptoas.GetTOAs(["twoch_mid"], "example.gmodel", quiet=True)
+        gt.get_TOAs(fit_DM=True, fit_GM=True, quiet=True)
+        assert len(gt.TOA_list) == 3
+        # subint 1 carried subint 0's flags with GM zeroed: no GM error
+        assert gt.GM_errs[0][1] == 0.0 and gt.GM_errs[0][0] > 0.0 and gt.GM_errs[0][2] > 0.0
+        assert gt.DM_errs[0][1] > 0.0
+        gt2 = pptoas.GetTOAs(["twoch_first"], "example.gmodel", quiet=True)
+        with pytest.raises(UnboundLocalError):
+            gt2.get_TOAs(fit_DM=True, fit_GM=True, quiet=True)
+    finally:
+        os.chdir(cwd)

@@ -1,8 +1,8 @@
 #!/bin/bash
 # Round-3 profile set at HEAD, one config per call:
 #   tools/profile_r03.sh TAG CONFIG [NSUB_PMC]
-# 1. bench line (HIP-event kernel times), 2. rocprofv3 --kernel-trace --stats
-# of the same command, 3. separate --pmc passes: FETCH_SIZE, WRITE_SIZE and
+# 1. bench line (HIP-event kernel times, caller legs), 2. rocprofv3
+# --kernel-trace --stats of the headline alone (--no-legs), 3. separate --pmc passes: FETCH_SIZE, WRITE_SIZE and
 # three SQ sets (instruction mix, waits, LDS, fp64 VALU / MFMA).
 # Every GPU step has its own time limit; the script stops at the first failure.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -16,10 +16,10 @@ cd /tmp || exit 1
 B="$R/bench.py --config $CFG"
 timeout -k 10 400 python3 $B --steps 5 --warmup 2 --cpu-sample 0 > $O/bench.log 2>&1 || { echo "bench failed"; tail -5 $O/bench.log; exit 1; }
 tail -1 $O/bench.log
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 $B --steps 5 --warmup 2 --cpu-sample 0 > $O/trace.log 2>&1 || { echo "trace failed"; tail -5 $O/trace.log; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 $B --steps 5 --warmup 2 --cpu-sample 0 --no-legs > $O/trace.log 2>&1 || { echo "trace failed"; tail -5 $O/trace.log; exit 1; }
 find $O/trace -name "*kernel_stats.csv" -exec head -8 {} \;
 pmc() {  # pmc NAME "COUNTERS" NSUB
-  timeout -s KILL 150 rocprofv3 --pmc $2 -d $O/pmc_$1 -o run --output-format csv -- python3 $B --nsub $3 --steps 1 --warmup 0 --cpu-sample 0 --no-timing > $O/pmc_$1.log 2>&1 || { echo "pmc $1 failed"; tail -3 $O/pmc_$1.log; return 1; }
+  timeout -s KILL 150 rocprofv3 --pmc $2 -d $O/pmc_$1 -o run --output-format csv -- python3 $B --nsub $3 --steps 1 --warmup 0 --cpu-sample 0 --no-timing --no-legs > $O/pmc_$1.log 2>&1 || { echo "pmc $1 failed"; tail -3 $O/pmc_$1.log; return 1; }
   echo "pmc $1 ok"
 }
 NF=${4:-0}
