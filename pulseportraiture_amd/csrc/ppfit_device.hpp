@@ -68,8 +68,10 @@ __device__ __forceinline__ double2 turn_phasor(double k, double phi) {
 template <int CTRL>
 __device__ __forceinline__ double dpp_mov(double v) {
   const unsigned long long u = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, 0xF, 0xF, false);
+  // bound_ctrl: a lane whose source is out of the row reads 0 (row_shr);
+  // every lane is written, so no old value has to be materialised first
+  const int lo = __builtin_amdgcn_mov_dpp((int)(unsigned)u, CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(unsigned)(u >> 32), CTRL, 0xF, 0xF, true);
   return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
 // value of the lane in the other 16-lane row of the pair (O = 16) / other half-wave (O = 32)
