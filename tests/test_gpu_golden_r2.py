@@ -256,21 +256,24 @@ def test_fit_full_r2_tnc(eng, golden, ic):
         assert {rc, ref_rc} <= CONVERGED, (rc, ref_rc)
     if ref_rc == 3:
         assert rc == 3 and int(r["nfev"][0]) == int(f[k + "nfeval"])
-    # TNC stops on |f_n - f_(n-1)| <= sqrt(eps) (scaled): the reference's own
-    # end point moves when its start moves by a few ulps (tnc_floor.npz).  The
-    # bar is north_star's 1e-3 sigma or twice that measured floor.
-    floor = golden("tnc_floor.npz")[k + "param_floor"]
-    tol = np.maximum(1e-3, 2.0 * floor)
+    # A converged fit ends within north_star's 1e-3 sigma of the reference's
+    # end point.  A fit stopped by maxfun (3) is not converged: its end point
+    # moves by sigmas when the start moves by ulps (tnc_floor.npz), so it is
+    # compared at equal evaluation counts along the reference's trajectory
+    # instead (tests/test_gpu_solver_traj.py).
     flags = [int(v) for v in f[k + "flags"]]
     ref = {key: float(f[k + key]) for key in ["phi", "phi_err", "nu_DM", "nu_GM"]}
     p = r["params"][0]
-    assert phase_gap(p[0], p[1], p[2], r["nu_out"][0][0], r["nu_out"][0][1], ref,
-                     float(f["P"])) <= tol[0]
+    gaps = [phase_gap(p[0], p[1], p[2], r["nu_out"][0][0], r["nu_out"][0][1], ref,
+                      float(f["P"]))]
     for i, nm in enumerate(["DM", "GM", "tau", "alpha"], start=1):
         if flags[i]:
             sig = float(f[k + nm + "_err"])
-            assert abs(p[i] - float(f[k + nm])) <= tol[i] * sig, (nm, p[i], float(f[k + nm]), sig)
+            gaps.append(abs(p[i] - float(f[k + nm])) / sig)
             assert r["param_errs"][0][i] == pytest.approx(sig, rel=1e-3 if ref_rc == 3 else 1e-5)
+    print("TNC case %d: |dx| / sigma %s" % (ic, ", ".join("%.1e" % g for g in gaps)))
+    if ref_rc != 3:
+        assert max(gaps) <= 1e-3, gaps
     assert r["red_chi2"][0] == pytest.approx(float(f[k + "red_chi2"]), rel=1e-6)
     print("TNC case %d: status %d (reference %d), nfev %d (reference %d)" % (
         ic, rc, ref_rc, int(r["nfev"][0]), int(f[k + "nfeval"])))
@@ -288,12 +291,15 @@ def test_legacy_fit_portrait_tnc(eng, golden, ic):
     ref_rc = int(g[k + "return_code"])
     if r.return_code != ref_rc:
         assert {r.return_code, ref_rc} <= CONVERGED, (r.return_code, ref_rc)
-    fl = golden("tnc_floor.npz")  # the reference's own ulp-restart spread
-    tphi = max(1e-3, 2.0 * float(fl[k + "phase_floor"]))
-    tdm = max(1e-3, 2.0 * float(fl[k + "DM_floor"]))
-    dphi = abs(r.phase - float(g[k + "phase"])) / float(g[k + "phase_err"])
-    assert dphi <= tphi, (dphi, tphi)
-    assert abs(r.DM - float(g[k + "DM"])) <= tdm * float(g[k + "DM_err"])
+    # phases compared at the reference's zero-covariance frequency (each fit
+    # reports its own); north_star's 1e-3 sigma
+    from tests._compare import phi_at
+    ph = phi_at(r.phase, r.DM, 0.0, r.nu_ref, np.inf, float(g[k + "nu_ref"]), np.inf, P0)
+    d = abs(ph - float(g[k + "phase"]))
+    dphi = min(d, 1.0 - d) / float(g[k + "phase_err"])
+    ddm = abs(r.DM - float(g[k + "DM"])) / float(g[k + "DM_err"])
+    print("legacy TNC %d: |dphi| / sigma %.1e, |dDM| / sigma %.1e" % (ic, dphi, ddm))
+    assert dphi <= 1e-3 and ddm <= 1e-3, (dphi, ddm)
     for key in ["phase_err", "DM_err", "red_chi2", "snr"]:
         assert r[key] == pytest.approx(float(g[k + key]), rel=1e-6), key
     assert r.nu_ref == pytest.approx(float(g[k + "nu_ref"]), rel=1e-7)

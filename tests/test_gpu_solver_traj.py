@@ -1,0 +1,158 @@
+"""The device TNC and Newton-CG solvers on the reference's own trajectories.
+
+tests/golden/solver_traj_r3.npz holds every objective evaluation (point and
+value, in call order) of the reference's TNC fits (fit_portrait_full with
+get_TOAs' bounds, pptoaslib.py:1005-1007; legacy pplib.fit_portrait,
+pplib.py:2144-2148) and Newton-CG fit (pptoaslib.py:1003-1004), recorded by
+tests/golden/make_golden_traj.py.  The device solver writes the same record
+(ppf_set_trace).  What is held:
+
+* the evaluations before the first step -- the start and the gradient
+  differences TNC takes there -- are the reference's points (1e-12 sigma);
+* from the first step on the points differ by the ulp-level difference of
+  the device's f and g from numpy's, amplified by the finite-difference
+  Hessian products of TNC (1/eps): 1e-9..1e-6 sigma after one step.  Along
+  the whole trajectory, compared at equal evaluation counts, the device stays
+  within 1e-2 sigma of the reference, and a fit that converges (status 1, 2
+  or 4 for both) ends within 1e-3 sigma of the reference's end point;
+* where one of the two runs more evaluations than the other, the extra ones
+  are spent at the floor: their f (chi^2 up to a constant) is within 1e-6 of
+  the shorter run's last f, a movement below 1.4e-3 sigma.  (tools/solver_replay.py shows the other half: fed
+  the device's own f and g, scipy's TNC / Newton-CG restated in
+  tools/tnc_model.py / ncg_model.py asks for exactly the device's points.)
+
+Every comparison prints the measured |dx| / sigma.
+"""
+import numpy as np
+import pytest
+
+from tests.conftest import GOLDEN
+from tests.golden_consts import P0
+
+pytestmark = pytest.mark.gpu
+
+FIT_CASES = ["f6", "f7", "f8", "f9", "f10"]
+LEGACY_CASES = ["l0", "l1"]
+
+
+@pytest.fixture(scope="module")
+def eng():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from pulseportraiture_amd.engine import get_engine
+    return get_engine(0)
+
+
+def _load(name):
+    import os
+    return np.load(os.path.join(GOLDEN, name))
+
+
+def _case(tag):
+    if tag.startswith("l"):
+        z = _load("legacy_fit_portrait.npz")
+        k = tag + "_"
+        return dict(data=z[k + "data"], model=z[k + "model"], freqs=z[k + "freqs"], P=P0,
+                    errs=z[k + "errs"], init=list(z[k + "init"]) + [0.0, 0.0, 0.0],
+                    nu=float(z[k + "nu_fit"]), flags=[1, 1, 0, 0, 0], log10=False, option=0,
+                    bounds=[(None, None)] * 5, method="TNC-legacy",
+                    sig=np.array([float(z[k + "phase_err"]), float(z[k + "DM_err"]), 1, 1, 1]),
+                    end=np.array([float(z[k + "phase"]), float(z[k + "DM"]), 0, 0, 0]),
+                    rc=int(z[k + "return_code"]), nfev=int(z[k + "nfeval"]))
+    z = _load("fit_full_r2.npz")
+    k = tag + "_"
+    b = z[k + "bounds"]
+    names = ["phi", "DM", "GM", "tau", "alpha"]
+    return dict(data=z[k + "data"], model=z[k + "model"], freqs=z[k + "freqs"], P=float(z["P"]),
+                errs=z[k + "errs"], init=list(z[k + "init"]), nu=float(z[k + "nu_fit"]),
+                flags=[int(v) for v in z[k + "flags"]], log10=bool(z[k + "log10"]),
+                option=int(z[k + "option"]), method=str(z[k + "method"]),
+                bounds=[tuple(None if np.isnan(v) else float(v) for v in row) for row in b],
+                sig=np.array([float(z[k + n + "_err"]) for n in names]),
+                end=None, rc=int(z[k + "return_code"]), nfev=int(z[k + "nfeval"]))
+
+
+def _device(eng, c, cap=512):
+    import torch
+    buf = torch.full((1, cap, 32), float("nan"), dtype=torch.float64, device=eng.device)
+    eng.set_trace(buf, cap)
+    try:
+        out = eng.fit_batch(c["data"], c["model"], c["freqs"], c["P"], c["init"], c["flags"],
+                            nu_fit=[c["nu"]] * 3, errs=c["errs"], log10_tau=c["log10"],
+                            option=c["option"], method=c["method"], bounds=c["bounds"])
+        torch.cuda.synchronize()
+    finally:
+        eng.set_trace(None, 0)
+    rec = buf[0].cpu().numpy()
+    rec = rec[~np.isnan(rec[:, 27])]
+    res = {k: v.cpu().numpy()[0] for k, v in out.items() if not k.startswith("_")}
+    return res, rec[rec[:, 26] == 1.0]  # the evaluations scipy counts in nfev
+
+
+@pytest.mark.parametrize("tag", FIT_CASES + LEGACY_CASES)
+def test_solver_follows_reference_trajectory(eng, tag):
+    tr = _load("solver_traj_r3.npz")
+    xr, fr = tr[tag + "_x"], tr[tag + "_f"]
+    c = _case(tag)
+    res, rec = _device(eng, c)
+    xd, fd = rec[:, :5], rec[:, 5]
+    assert len(xr) == c["nfev"] and int(res["nfev"]) == len(xd)
+    fl = np.array(c["flags"], bool)
+    sig = np.where(c["sig"] > 0, c["sig"], 1.0)
+    n = min(len(xd), len(xr))
+    dx = np.array([(np.abs(xd[i] - xr[i]) / sig)[fl].max() for i in range(n)])
+    # the first step: the first evaluation whose f moves by more than 1e-4
+    # (relative) from the start (before it: the start point and TNC's
+    # gradient-difference points around it)
+    step = next(i for i in range(1, len(fr)) if abs(fr[i] - fr[0]) > 1e-4 * abs(fr[0]))
+    print("%s %s: nfev %d (reference %d), status %d (reference %d); |dx|/sigma before the "
+          "first step (eval %d) %.1e, after it %.1e, max over %d common evals %.1e, at the "
+          "last common eval %.1e" % (tag, c["method"], len(xd), len(xr), int(res["status"]),
+                                      c["rc"], step, dx[:step].max(), dx[step], n, dx.max(),
+                                      dx[n - 1]))
+    assert dx[:step].max() <= 1e-12
+    assert dx[step] <= 1e-5
+    assert dx.max() <= 1e-2
+    # extra evaluations of the longer run sit at the floor: f (a chi^2 up to
+    # a constant) moves by < 1e-6 there, i.e. by < 1.4e-3 sigma of movement
+    for who, f_, m in (("device", fd, len(xd)), ("reference", fr, len(xr))):
+        if m > n:
+            tail = np.abs(f_[n:] - f_[n - 1])
+            print("   %s's %d extra evaluations: |f - f_last| <= %.1e (|f| %.3g)" % (
+                who, m - n, tail.max(), abs(f_[n - 1])))
+            assert tail.max() <= 1e-6
+    if c["rc"] == 3:  # maxfun: compared at equal nfev above, no end point
+        assert int(res["status"]) == 3 and len(xd) == len(xr)
+
+
+@pytest.mark.parametrize("tag", ["f6", "f8", "f9", "f10"] + LEGACY_CASES)
+def test_converged_end_point_within_1e3_sigma(eng, tag):
+    """Converged TNC / Newton-CG fits end within 1e-3 sigma of the reference
+    (phase compared at the reference's output frequency)."""
+    from tests._compare import CONVERGED, phase_gap
+    c = _case(tag)
+    res, _ = _device(eng, c)
+    assert {int(res["status"]), c["rc"]} <= CONVERGED
+    p = res["params"]
+    if tag.startswith("l"):
+        from pulseportraiture_amd import pplib
+        from tests._compare import phi_at
+        z = _load("legacy_fit_portrait.npz")
+        r = pplib.fit_portrait(c["data"], c["model"], c["init"][:2], P0, c["freqs"], c["nu"],
+                               None, c["errs"])
+        # the phase is reported at each fit's own zero-covariance frequency:
+        # compare it at the reference's
+        ph = phi_at(r.phase, r.DM, 0.0, r.nu_ref, np.inf, float(z[tag + "_nu_ref"]), np.inf, P0)
+        d = abs(ph - c["end"][0])
+        gaps = [min(d, 1.0 - d) / c["sig"][0], abs(r.DM - c["end"][1]) / c["sig"][1]]
+    else:
+        z = _load("fit_full_r2.npz")
+        k = tag + "_"
+        ref = {key: float(z[k + key]) for key in ["phi", "phi_err", "nu_DM", "nu_GM"]}
+        gaps = [phase_gap(p[0], p[1], p[2], res["nu_out"][0], res["nu_out"][1], ref, c["P"])]
+        for i, nm in enumerate(["DM", "GM", "tau", "alpha"], start=1):
+            if c["flags"][i]:
+                gaps.append(abs(p[i] - float(z[k + nm])) / float(z[k + nm + "_err"]))
+    print("%s: end point |dx| / sigma %s" % (tag, ", ".join("%.1e" % g for g in gaps)))
+    assert max(gaps) <= 1e-3

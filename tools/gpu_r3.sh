@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 measure cycle: GPU suite, solver trajectories vs the reference,
+# Round-3 measure cycle: GPU suite, the solver-trajectory tests verbose,
 # headline bench (no legs).  usage: tools/gpu_r3.sh TAG
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" || exit 1
@@ -9,8 +9,8 @@ timeout -k 10 700 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-me
 rc=$?
 tail -4 gpurun_out/${T}_tests.log
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit 1
-timeout -k 10 300 python -u tools/traj_compare.py gpurun_out/${T}_traj.json > gpurun_out/${T}_traj.log 2>&1 || { echo "traj failed"; tail -5 gpurun_out/${T}_traj.log; exit 1; }
-grep '^{' gpurun_out/${T}_traj.log
+timeout -k 10 300 python -u -m pytest tests/test_gpu_solver_traj.py -m gpu -q -s --timeout 120 --timeout-method thread > gpurun_out/${T}_traj.log 2>&1 || [ $? -eq 1 ] || { echo "traj tests crashed"; exit 1; }
+grep -E "nfev|end point|extra" gpurun_out/${T}_traj.log
 timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --cpu-sample 0 --no-legs > gpurun_out/${T}_bench.log 2>&1 || { echo "bench failed"; tail -5 gpurun_out/${T}_bench.log; exit 1; }
 python3 - "$T" <<'PY'
 import json, sys
