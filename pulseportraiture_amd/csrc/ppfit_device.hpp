@@ -602,12 +602,18 @@ __device__ __forceinline__ void rfft_pair_v(double2 zk, double2 znk, double2 w, 
 //      in registers, twiddle W_1024^{j r}, one LDS transpose;
 //   B  lane (j0 = l & 3, r = l >> 2) takes Y_{j0 + 4 t}[r], 16-point DFT over
 //      t in registers, twiddle W_64^{j0 s};
-//   C  4-point DFT over j0 across each lane quad (two DPP radix-2 steps);
+//   C  the twiddled values go through LDS once more (slot 64 s + 16 j0 +
+//      (rr ^ 2 j0): conflict-free for the quad-strided writes and for the
+//      reads), lane (rr = l & 15, q = l >> 4) takes the four j0 of s = 4 q + c
+//      (c < 4) and does the 4-point DFTs over j0 in registers (radix4: the
+//      -i is a component swap, no cross-lane moves or lane selects);
 // then Z_k goes to LDS once, in the padded order P(k) = k + 4 (k >> 8) that
-// keeps the quad-strided writes and the (k, N - k) reads of the real-FFT
-// post-processing free of bank conflicts.  Two LDS round trips per row
-// instead of the Stockham path's six.  Twiddles are exact table values
-// (W^{4a+b} = W^{4a} W^b: at most one rounding).
+// keeps the writes (8 consecutive rr per group) and the (k, N - k) reads of
+// the real-FFT post-processing free of bank conflicts.  Three LDS round trips
+// per row instead of the Stockham path's six.  Twiddles are exact table
+// values (W^{4a+b} = W^{4a} W^b: at most one rounding).  Stage C forms
+// exactly the sums of the former DPP radix-2 pair (a0 + a2, a0 - a2, -i(a1 -
+// a3), ...), so the spectrum is bitwise unchanged.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ double2 mul_negi(double2 a) { return cmk(a.y, -a.x); }
 
@@ -682,19 +688,21 @@ __device__ __forceinline__ void fft1024_wave(const double (&x)[16], const double
   for (int i = 1; i < 4; ++i) { lo[i] = t.c[i - 1][j0]; hi[i] = t.d[i - 1][j0]; }
   dft16(v);
   fft_sync<true>();
-  const bool p = (lane & 2) != 0, q = (lane & 1) != 0;
-  const int u = (p ? 1 : 0) + (q ? 2 : 0);
-  // radix-2 steps as fma(+-1, own, partner): o - a on the upper lane, a + o on
-  // the lower one, each rounded once exactly as the add / sub it replaces
-  const double sp = p ? -1.0 : 1.0, sq = q ? -1.0 : 1.0;
 #pragma unroll
-  for (int s = 0; s < 16; ++s) {
-    const double2 a = s ? cmul(v[dft16_pos(s)], tw_pow(s, lo, hi)) : v[0];
-    const double2 o = cmk(dpp_mov<0x4E>(a.x), dpp_mov<0x4E>(a.y));  // lane ^ 2
-    double2 b = cmk(fma(sp, a.x, o.x), fma(sp, a.y, o.y));
-    if (p && q) b = mul_negi(b);
-    const double2 o2 = cmk(dpp_mov<0xB1>(b.x), dpp_mov<0xB1>(b.y));  // lane ^ 1
-    buf[rr + 16 * s + 260 * u] = cmk(fma(sq, b.x, o2.x), fma(sq, b.y, o2.y));
+  for (int s = 0; s < 16; ++s)
+    buf[64 * s + 16 * j0 + (rr ^ (2 * j0))] = s ? cmul(v[dft16_pos(s)], tw_pow(s, lo, hi)) : v[0];
+  fft_sync<true>();
+  const int r2 = lane & 15, q4 = lane >> 4;
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[4 * c + j] = buf[64 * (4 * q4 + c) + 16 * j + (r2 ^ (2 * j))];
+  fft_sync<true>();  // all reads done before Z overwrites their slots
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    radix4<false>(v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) buf[r2 + 16 * (4 * q4 + c) + 260 * u] = v[4 * c + u];
   }
   fft_sync<true>();
 }
