@@ -63,7 +63,7 @@ PMC_TRAFFIC = {"headline": os.path.join(ROOT, "profiles", "r03_pmc_traffic_headl
                "scattering": os.path.join(ROOT, "profiles", "r03_pmc_traffic_scattering.json")}
 KERNEL_SYMBOL = {"solve": "k_scat_sweep", "data_xspec": "k_data_xspec<10>",
                  "post": "k_post<false>", "guess": "k_guess_w", "moments": "k_moments<4>",
-                 "fit_taylor": "k_fit_taylor"}
+                 "fit_taylor": "k_fit_taylor<true>"}
 # fp64 operations of one scattering cell evaluation as cells_scat forms them
 # (ppfit_fit.hip: phasor step 6, W 6, B 13, f 8, g1 9, three conjugate
 # products 18, ten accumulations 30; the hardware reciprocal not counted)

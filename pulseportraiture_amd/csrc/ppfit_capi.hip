@@ -131,6 +131,22 @@ int moments_u() {
   return u;
 }
 
+// first moment pass inside k_fit_taylor (default) or its own k_moments
+// launch (A/B knob PPF_FUSE_MOMENTS=0)
+bool fuse_moments() {
+  static const bool f = [] {
+    const char* e = getenv("PPF_FUSE_MOMENTS");
+    return !(e && atoi(e) == 0);
+  }();
+  return f;
+}
+void launch_fit_taylor(dim3 g, size_t lds, hipStream_t st, const FitArgs& fa) {
+  if (fuse_moments())
+    hipLaunchKernelGGL(k_fit_taylor<true>, g, dim3(kBlock), lds, st, fa);
+  else
+    hipLaunchKernelGGL(k_fit_taylor<false>, g, dim3(kBlock), lds, st, fa);
+}
+
 int vpow_table(ppf_ctx* ctx, int nbin, const double2** out) {
   const int l = ilog2_exact(nbin);
   if (!ctx->vp[l]) {
@@ -599,16 +615,17 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
               hipLaunchKernelGGL(k_guess, dim3(n), dim3(kBlock), d->guess ? lds_guess : 0, st, fp);
             }))
           return r;
-        if (int r = timed_on(ctx, PPF_K_MOMENTS, st, [&] {
-              const dim3 g(n, (nchan + 16 * kWaves - 1) / (16 * kWaves));
-              if (moments_u() == 4)
-                hipLaunchKernelGGL(k_moments<4>, g, dim3(kBlock), 0, st, fp);
-              else
-                hipLaunchKernelGGL(k_moments<8>, g, dim3(kBlock), 0, st, fp);
-            }))
-          return r;
+        if (!fuse_moments())
+          if (int r = timed_on(ctx, PPF_K_MOMENTS, st, [&] {
+                const dim3 g(n, (nchan + 16 * kWaves - 1) / (16 * kWaves));
+                if (moments_u() == 4)
+                  hipLaunchKernelGGL(k_moments<4>, g, dim3(kBlock), 0, st, fp);
+                else
+                  hipLaunchKernelGGL(k_moments<8>, g, dim3(kBlock), 0, st, fp);
+              }))
+            return r;
         if (int r = timed_on(ctx, PPF_K_FIT_TAYLOR, st, [&] {
-              hipLaunchKernelGGL(k_fit_taylor, dim3(n), dim3(kBlock), lds_taylor, st, fp);
+              launch_fit_taylor(dim3(n), lds_taylor, st, fp);
             }))
           return r;
         if (int r = timed_on(ctx, PPF_K_POST, st, [&] {
@@ -686,17 +703,20 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
       }
     }
     if (taylor) {
-      if (int r = timed(ctx, PPF_K_MOMENTS, [&] {
-            const dim3 g(nc, (nchan + 16 * kWaves - 1) / (16 * kWaves));
-            // steps in flight per wave (tuning knob PPF_MOMENTS_U = 4 / 8)
-            if (moments_u() == 4)
-              hipLaunchKernelGGL(k_moments<4>, g, dim3(kBlock), 0, ctx->stream, fa);
-            else
-              hipLaunchKernelGGL(k_moments<8>, g, dim3(kBlock), 0, ctx->stream, fa);
-          }))
-        return r;
+      // the first moment pass inside k_fit_taylor (default), or its own
+      // launch (PPF_FUSE_MOMENTS=0)
+      if (!fuse_moments())
+        if (int r = timed(ctx, PPF_K_MOMENTS, [&] {
+              const dim3 g(nc, (nchan + 16 * kWaves - 1) / (16 * kWaves));
+              // steps in flight per wave (tuning knob PPF_MOMENTS_U = 4 / 8)
+              if (moments_u() == 4)
+                hipLaunchKernelGGL(k_moments<4>, g, dim3(kBlock), 0, ctx->stream, fa);
+              else
+                hipLaunchKernelGGL(k_moments<8>, g, dim3(kBlock), 0, ctx->stream, fa);
+            }))
+          return r;
       if (int r = timed(ctx, PPF_K_FIT_TAYLOR, [&] {
-            hipLaunchKernelGGL(k_fit_taylor, dim3(nc), dim3(kBlock), lds_taylor, ctx->stream, fa);
+            launch_fit_taylor(dim3(nc), lds_taylor, ctx->stream, fa);
           }))
         return r;
     }

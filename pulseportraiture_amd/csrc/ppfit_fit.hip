@@ -500,7 +500,7 @@ __device__ __forceinline__ int flag_mask(const FitArgs& a) {
 //   gc = -2 C C1 / S,  hc = -2 (C C2 + C1^2) / S,
 // so each lane carries 10 running sums over its channel groups and the wave
 // reduces them once, instead of 21 reductions per group.
-__device__ void sweep_taylor0(const FitArgs& a, const Meta& m, const double* prm,
+__device__ __forceinline__ void sweep_taylor0(const FitArgs& a, const Meta& m, const double* prm,
                               double* acc_slot, double* out, double (*red)[48],
                               const TaylorSrc& ts) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -595,7 +595,7 @@ __device__ void sweep_taylor0(const FitArgs& a, const Meta& m, const double* prm
 // the end, instead of NP wave reductions per channel group.
 // [j0, j1) (multiples of 8 but the end): the fitted channels this block sums.
 template <int MODE, bool SCAT>
-__device__ void sweep(const FitArgs& a, const Meta& m, int c, int s, const double* prm,
+__device__ __forceinline__ void sweep(const FitArgs& a, const Meta& m, int c, int s, const double* prm,
                       const double* refs, double P, double* acc_slot, double* out,
                       double (*red)[48], const TaylorSrc& ts, double (*lrow)[48] = nullptr,
                       int j0 = 0, int j1 = 1 << 30, double* gpart = nullptr) {

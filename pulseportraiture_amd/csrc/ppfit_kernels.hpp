@@ -475,6 +475,7 @@ constexpr int kScatPart = 24;  // split scattering sweep partial: f, g[5], H pai
 __global__ void k_scat_sweep(FitArgs a, double* part, int split, int init);
 __global__ void k_scat_step(FitArgs a, const double* part, int split, int init, int* active);
 __global__ void k_model_mean(const double2* M, double2* Mmean, int nchan, int NHP);
+template <bool MOM>
 __global__ void k_fit_taylor(FitArgs a);
 template <int U>
 __global__ void k_moments(FitArgs a);
