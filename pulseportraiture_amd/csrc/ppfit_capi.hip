@@ -147,6 +147,16 @@ void launch_fit_taylor(dim3 g, size_t lds, hipStream_t st, const FitArgs& fa) {
     hipLaunchKernelGGL(k_fit_taylor<false>, g, dim3(kBlock), lds, st, fa);
 }
 
+// split scattering solve: below this many running subints the sweeps take
+// one 8-channel group per wave (A/B knob PPF_SCAT_TAIL; 0 keeps the split)
+int scat_tail_subints() {
+  static const int v = [] {
+    const char* e = getenv("PPF_SCAT_TAIL");
+    return e ? atoi(e) : 512;
+  }();
+  return v;
+}
+
 int vpow_table(ppf_ctx* ctx, int nbin, const double2** out) {
   const int l = ilog2_exact(nbin);
   if (!ctx->vp[l]) {
@@ -683,10 +693,15 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
       // the running count is read back every kCheck iterations (a finished
       // subint's blocks exit at once, so the extra launches are cheap)
       constexpr int kCheck = 4;
+      // once few subints are left (the tail of slow fits), each sweep is
+      // spread over more blocks: one 8-channel group per wave.  The group
+      // partials, and so every result, do not depend on the split.
+      int cur = split;
+      const int split_tail = std::max(split, std::min(32, (nchan + 31) / 32));
       for (int it = 0, init = 1;; ++it, init = 0) {
         if (int r = timed(ctx, PPF_K_SOLVE, [&] {
-              hipLaunchKernelGGL(k_scat_sweep, dim3(nc, split), dim3(kBlock), lds_meta,
-                                 ctx->stream, fa, part, split, init);
+              hipLaunchKernelGGL(k_scat_sweep, dim3(nc, cur), dim3(kBlock), lds_meta,
+                                 ctx->stream, fa, part, cur, init);
             }))
           return r;
         HIPCHK(ctx, hipMemsetAsync(active, 0, sizeof(int), ctx->stream));
@@ -700,6 +715,7 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
                                    ctx->stream));
         HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
         if (*ctx->active_h == 0 || it > 1001) break;  // trust-ncg stops at 1000 iterations
+        if (*ctx->active_h < scat_tail_subints()) cur = split_tail;
       }
     }
     if (taylor) {

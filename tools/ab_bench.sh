@@ -14,7 +14,7 @@ for v in "$@"; do
     env:*) envs=${v#env:} ;;
     *) export PPF_LIB=$R/pulseportraiture_amd/variants/libppfit_$v.so ;;
   esac
-  env $envs timeout -k 10 200 python3 -u bench.py --steps 5 --warmup 2 --cpu-sample 0 --no-legs > gpurun_out/${T}_$v.log 2>&1 || { echo "$v failed"; tail -3 gpurun_out/${T}_$v.log; exit 1; }
+  env $envs timeout -k 10 300 python3 -u bench.py ${BENCH_ARGS:---steps 5 --warmup 2} --cpu-sample 0 --no-legs > gpurun_out/${T}_$v.log 2>&1 || { echo "$v failed"; tail -3 gpurun_out/${T}_$v.log; exit 1; }
   python3 - gpurun_out/${T}_$v.log $v <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
