@@ -118,7 +118,7 @@ def fit_portraits_batch(data, model, init, P, freqs, nu_fits=None, nu_outs=None,
     if not to_host:
         return out
     res = {k: v.cpu().numpy() for k, v in out.items() if not k.startswith("_")}
-    res["duration"] = np.full(len(res["chi2"]), (time.time() - t0) / len(res["chi2"]))
+    res["duration"] = np.full(len(res["chi2"]), (time.time() - t0) / max(len(res["chi2"]), 1))
     return res
 
 
