@@ -140,7 +140,14 @@ __device__ __forceinline__ void block_sum_vec(double (&v)[N], double (*red)[48])
 // The row is streamed with the next U harmonics' loads in flight while the
 // current U are accumulated (software pipelining: one HBM latency per row,
 // not one per step); the accumulation order is unchanged.
-constexpr int kPipe = 4;  // divides the 32-step re-seed period
+constexpr int kPipe = 4;
+
+// Diagnostic builds only (tools/build_variant.py -DPPF_PROBE_SCAT=N, timing
+// of the scattering sweep's parts; results are wrong): 1 skips the
+// per-channel f/g/H terms, 2 the cell loop.
+#ifndef PPF_PROBE_SCAT
+#define PPF_PROBE_SCAT 0
+#endif  // divides the 32-step re-seed period
 
 __device__ __forceinline__ void cells_phase(const double2* __restrict__ Xr, int J, int h,
                                             double phif, double* acc) {
@@ -363,6 +370,78 @@ __device__ __forceinline__ double Hn_(const ChanDeriv& d, int i, int j) {
   return -2.0 * (C * C / S) *
          ((d2C_(d, i, j) / C) - (0.5 * d2S_(d, i, j) / S) + (dCi * dCj / (C * C)) +
           (dSi * dSj / (S * S)) - ((dCi * dSj) + (dSi * dCj)) / (C * S));
+}
+
+// The same terms with a lane-varying parameter index (i <= j): each operand
+// chosen by selects, every case formed with the expression of the constant-
+// index version, each operation rounded on its own as numpy rounds the
+// reference's (pptoaslib.py:588-628; no contraction into fma).  Each pick selects
+// between opaque copies: a select between fields of one aggregate would fold
+// into a run-time-indexed load and keep the aggregate in scratch.
+__device__ __forceinline__ double opq(double x) {
+  asm("" : "+v"(x));
+  return x;
+}
+struct LanePick {
+  double ph0, ph1, ph2, ts0, ts1, t2a, t2b, t2c;
+  __device__ __forceinline__ double dph(int i) const {
+    const double a = opq(ph0), b = opq(ph1), c = opq(ph2);
+    return i == 0 ? a : (i == 1 ? b : c);
+  }
+  __device__ __forceinline__ double dts(int i) const {  // i = 3, 4
+    const double a = opq(ts0), b = opq(ts1);
+    return i == 4 ? b : a;
+  }
+  __device__ __forceinline__ double d2ts(int i, int j) const {
+    const double a = opq(t2a), b = opq(t2b), c = opq(t2c);
+    return (i == 3 && j == 3) ? a : ((i == 4 && j == 4) ? c : b);
+  }
+};
+__device__ __forceinline__ double dCr(const ChanDeriv& d, const LanePick& L, int i) {
+#pragma clang fp contract(off)
+  const double ph = d.C1 * L.dph(i);
+  const double sc = L.dts(i) * d.F1;
+  return i < 3 ? ph : sc;
+}
+__device__ __forceinline__ double dSr(const ChanDeriv& d, const LanePick& L, int i) {
+#pragma clang fp contract(off)
+  const double sc = 2.0 * L.dts(i) * d.SF;
+  return i < 3 ? 0.0 : sc;
+}
+__device__ __forceinline__ double d2Cr(const ChanDeriv& d, const LanePick& L, int i, int j) {
+#pragma clang fp contract(off)
+  const double pp = d.C2 * L.dph(i) * L.dph(j);
+  const double ps = L.dph(i) * L.dts(j) * d.F1p;
+  const double ss = L.dts(i) * L.dts(j) * d.G1 + L.d2ts(i, j) * d.F1;
+  return j < 3 ? pp : (i < 3 ? ps : ss);
+}
+__device__ __forceinline__ double d2Sr(const ChanDeriv& d, const LanePick& L, int i, int j) {
+#pragma clang fp contract(off)
+  const double ss = 2.0 * (L.dts(i) * L.dts(j) * (d.SFF + d.SG) + L.d2ts(i, j) * d.SF);
+  return i < 3 ? 0.0 : ss;
+}
+__device__ __forceinline__ double Hnr(const ChanDeriv& d, const LanePick& L, int i, int j) {
+#pragma clang fp contract(off)
+  const double C = d.C, S = d.S;
+  const double dCi = dCr(d, L, i), dCj = dCr(d, L, j), dSi = dSr(d, L, i), dSj = dSr(d, L, j);
+  return -2.0 * (C * C / S) *
+         ((d2Cr(d, L, i, j) / C) - (0.5 * d2Sr(d, L, i, j) / S) + (dCi * dCj / (C * C)) +
+          (dSi * dSj / (S * S)) - ((dCi * dSj) + (dSi * dCj)) / (C * S));
+}
+// out-slot t of a MODE-0 sweep for one channel (q = C^2 / S): 0 f, 1 + i
+// g_i, 6 + p H pair p; 0 for unfitted parameters and t >= 21
+__device__ __forceinline__ double mode0_term(const ChanDeriv& d, const LanePick& L, double q,
+                                             int t, int fm) {
+#pragma clang fp contract(off)
+  const int gi = min(max(t - 1, 0), 4);
+  const int p = min(max(t - 6, 0), 14);
+  const int pi = p < 5 ? 0 : (p < 9 ? 1 : (p < 12 ? 2 : (p < 14 ? 3 : 4)));
+  const int pj = p < 5 ? p : (p < 9 ? p - 4 : (p < 12 ? p - 7 : (p < 14 ? p - 9 : 4)));
+  const double gv = -q * (2.0 * dCr(d, L, gi) / d.C - dSr(d, L, gi) / d.S);
+  const double hv = Hnr(d, L, pi, pj);
+  const bool on = t == 0 || (t < 6 ? ((fm >> gi) & 1) : ((fm >> pi) & (fm >> pj) & 1));
+  const double v = t == 0 ? -q : (t < 6 ? gv : hv);
+  return (on && t < 21) ? v : 0.0;
 }
 
 // phi_n (pptoaslib.py:206-208), reduced to [0, 1)
@@ -612,6 +691,7 @@ __device__ __forceinline__ void sweep(const FitArgs& a, const Meta& m, int c, in
   const double tau_lin = SCAT ? (log10_tau ? pow(10.0, prm[3]) : prm[3]) : 0.0;
   const bool scat = SCAT && tau_lin != 0.0;
   const int midx = a.model_idx ? a.model_idx[s] : 0;
+  const int fm = flag_mask(a);
   constexpr int NP = MODE == 0 ? 21 : 45;
   if (lane < NP) red[w][lane] = 0.0;
   double* myrow = lrow ? lrow[w * 8 + g8] : nullptr;
@@ -640,14 +720,48 @@ __device__ __forceinline__ void sweep(const FitArgs& a, const Meta& m, int c, in
       const double2* Xr = a.X + ((size_t)c * a.nchan + n) * a.NHP;
       const double* M2r = a.M2 + ((size_t)midx * a.nchan + n) * a.NHP;
       const double taun = tau_lin * pow(fr / refs[2], prm[4]);
-      cells_scat<4>(Xr, M2r, J, h, phif, taun, acc);
+      if (PPF_PROBE_SCAT == 2) {
+        for (int i = 0; i < NACC; ++i) acc[i] = 0.5 + taun * i;
+      } else {
+        cells_scat<4>(Xr, M2r, J, h, phif, taun, acc);
+      }
     }
 #pragma unroll
     for (int i = 0; i < NACC; ++i) acc[i] = group8_sum(acc[i]);
+    if constexpr (MODE == 0) {
+      if (!lrow) {
+        // f, g and H terms spread over each channel's 8 lanes: lane h forms
+        // out-slots h, h + 8, h + 16 (the channel's sums are on all 8 after
+        // group8_sum), then one chan8_sum per slot row sums the group's 8
+        // channels -- the additions wave_sum made on one lane's 21 terms, on
+        // the same operands, so every slot is bitwise as before
+        const double dpre[2] = {m.d1[jj], m.d2[jj]};
+        const ChanDeriv d = derive<SCAT>(acc, scat, m.pn[jj], m.iw2[jj], fr, prm, tau_lin, refs,
+                                         P, log10_tau, dpre);
+        const double q = d.C * d.C / d.S;
+        const LanePick L{d.dph[0], d.dph[1], d.dph[2], d.dts[0],
+                         d.dts[1], d.d2ts[0], d.d2ts[1], d.d2ts[2]};
+        if (h == 0 && valid) {
+          double* dst = acc_slot + (size_t)j * NACC;
+          for (int i = 0; i < NACC; ++i) dst[i] = acc[i];
+        }
+        const bool on = valid && !(SCAT && PPF_PROBE_SCAT == 1);
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          const double v = chan8_sum(on ? mode0_term(d, L, q, h + 8 * r, fm) : 0.0);
+          const int t = (lane & 7) + 8 * r;
+          if (lane >= 8 && lane < 16 && t < NP) {
+            if (gpart) gpart[(size_t)gi * kScatPart + t] = v;  // summed by the caller
+            else red[w][t] += v;
+          }
+        }
+        continue;
+      }
+    }
     double ct[NP];
 #pragma unroll
     for (int i = 0; i < NP; ++i) ct[i] = 0.0;
-    if (h == 0 && valid) {
+    if (h == 0 && valid && !(SCAT && PPF_PROBE_SCAT == 1)) {
       const double dpre[2] = {m.d1[j], m.d2[j]};
       const ChanDeriv d = derive<SCAT>(acc, scat, m.pn[j], m.iw2[j], fr, prm, tau_lin, refs, P,
                                        log10_tau, MODE == 0 ? dpre : nullptr);

@@ -46,7 +46,12 @@ def main():
         wb = max(write.get(k, [0.0]))
         res["kernels"][k] = {"read_bytes_per_launch": fb, "write_bytes_per_launch": wb,
                              "bytes_per_launch": fb + wb,
-                             "bytes_per_subint": (fb + wb) / nsub}
+                             "bytes_per_subint": (fb + wb) / nsub,
+                             # all launches of the run (chains such as the split
+                             # scattering solve launch k_scat_sweep many times a step)
+                             "launches": len(fetch.get(k, [])),
+                             "bytes_all_launches": 2.0 * sum(fetch.get(k, [0.0])) +
+                             sum(write.get(k, [0.0]))}
     json.dump(res, open(out, "w"), indent=1)
     for k, v in res["kernels"].items():
         print("%-22s read %.3e  write %.3e  per-subint %.4e" % (
