@@ -147,6 +147,14 @@ constexpr int kPipe = 4;
 // per-channel f/g/H terms, 2 the cell loop.
 #ifndef PPF_PROBE_SCAT
 #define PPF_PROBE_SCAT 0
+#endif
+// cells in flight per lane in the scattering sweep and k_scat_sweep's
+// workgroups per CU (launch bound); A/B knobs for diagnostic builds
+#ifndef PPF_SCAT_U
+#define PPF_SCAT_U 4
+#endif
+#ifndef PPF_SCAT_WG_PER_CU
+#define PPF_SCAT_WG_PER_CU 1
 #endif  // divides the 32-step re-seed period
 
 __device__ __forceinline__ void cells_phase(const double2* __restrict__ Xr, int J, int h,
@@ -723,7 +731,7 @@ __device__ __forceinline__ void sweep(const FitArgs& a, const Meta& m, int c, in
       if (PPF_PROBE_SCAT == 2) {
         for (int i = 0; i < NACC; ++i) acc[i] = 0.5 + taun * i;
       } else {
-        cells_scat<4>(Xr, M2r, J, h, phif, taun, acc);
+        cells_scat<PPF_SCAT_U>(Xr, M2r, J, h, phif, taun, acc);
       }
     }
 #pragma unroll
@@ -1464,7 +1472,7 @@ __device__ __forceinline__ bool scat_split_owner(const FitArgs& a, const SolveSt
   return a.method == PPF_METHOD_TRUST_NCG && st.scat != 0 && !st.sdone;
 }
 
-__global__ __launch_bounds__(kBlock) void k_scat_sweep(FitArgs a, double* part, int split,
+__global__ __launch_bounds__(kBlock, PPF_SCAT_WG_PER_CU) void k_scat_sweep(FitArgs a, double* part, int split,
                                                        int init) {
   extern __shared__ __align__(16) unsigned char dyn[];
   __shared__ SolveShared sh;
