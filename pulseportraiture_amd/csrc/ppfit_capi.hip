@@ -149,6 +149,16 @@ void launch_fit_taylor(dim3 g, size_t lds, hipStream_t st, const FitArgs& fa) {
 
 // split scattering solve: below this many running subints the sweeps take
 // one 8-channel group per wave (A/B knob PPF_SCAT_TAIL; 0 keeps the split)
+// the split scattering solve's iterations as hipGraph launches: opt-in
+// (PPF_SCAT_GRAPH=1) until measured; default one launch per kernel
+bool scat_graph() {
+  static const bool on = [] {
+    const char* e = getenv("PPF_SCAT_GRAPH");
+    return e && atoi(e) != 0;
+  }();
+  return on;
+}
+
 int scat_tail_subints() {
   static const int v = [] {
     const char* e = getenv("PPF_SCAT_TAIL");
@@ -698,18 +708,60 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
       // partials, and so every result, do not depend on the split.
       int cur = split;
       const int split_tail = std::max(split, std::min(32, (nchan + 31) / 32));
+      // after the first kCheck iterations, each group of kCheck is one
+      // hipGraph launch (the same kernels in the same order, captured once
+      // per call and split): fewer launch gaps between the short kernels
+      hipGraphExec_t gx[2] = {nullptr, nullptr};
+      auto graph_for = [&](int s, hipGraphExec_t* ex) -> int {
+        if (*ex) return PPF_OK;
+        // captured on the context's second queue (the context stream may be
+        // the legacy default stream, which cannot capture); launched on the
+        // context stream
+        if (!ctx->stream2)
+          HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
+        hipStream_t cs = ctx->stream2;
+        hipGraph_t g = nullptr;
+        HIPCHK(ctx, hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
+        for (int k = 0; k < kCheck; ++k) {
+          hipLaunchKernelGGL(k_scat_sweep, dim3(nc, s), dim3(kBlock), lds_meta, cs, fa, part, s,
+                             0);
+          (void)hipMemsetAsync(active, 0, sizeof(int), cs);
+          hipLaunchKernelGGL(k_scat_step, dim3(nc), dim3(64), 0, cs, fa, part, split, 0, active);
+        }
+        HIPCHK(ctx, hipStreamEndCapture(cs, &g));
+        const hipError_t e = hipGraphInstantiate(ex, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        if (e != hipSuccess)
+          return fail(ctx, PPF_ERR_DEVICE, "scattering solve graph: %s", hipGetErrorString(e));
+        return PPF_OK;
+      };
+      struct GraphFree {
+        hipGraphExec_t* g;
+        ~GraphFree() {
+          for (int i = 0; i < 2; ++i)
+            if (g[i]) (void)hipGraphExecDestroy(g[i]);
+        }
+      } gfree{gx};
       for (int it = 0, init = 1;; ++it, init = 0) {
-        if (int r = timed(ctx, PPF_K_SOLVE, [&] {
-              hipLaunchKernelGGL(k_scat_sweep, dim3(nc, cur), dim3(kBlock), lds_meta,
-                                 ctx->stream, fa, part, cur, init);
-            }))
-          return r;
-        HIPCHK(ctx, hipMemsetAsync(active, 0, sizeof(int), ctx->stream));
-        if (int r = timed(ctx, PPF_K_SOLVE, [&] {
-              hipLaunchKernelGGL(k_scat_step, dim3(nc), dim3(64), 0, ctx->stream, fa, part, split,
-                                 init, active);
-            }))
-          return r;
+        if (scat_graph() && it >= kCheck && it % kCheck == 0 && it + kCheck - 1 <= 1001) {
+          hipGraphExec_t* ex = &gx[cur == split ? 0 : 1];
+          if (int r = graph_for(cur, ex)) return r;
+          if (int r = timed(ctx, PPF_K_SOLVE, [&] { (void)hipGraphLaunch(*ex, ctx->stream); }))
+            return r;
+          it += kCheck - 1;
+        } else {
+          if (int r = timed(ctx, PPF_K_SOLVE, [&] {
+                hipLaunchKernelGGL(k_scat_sweep, dim3(nc, cur), dim3(kBlock), lds_meta,
+                                   ctx->stream, fa, part, cur, init);
+              }))
+            return r;
+          HIPCHK(ctx, hipMemsetAsync(active, 0, sizeof(int), ctx->stream));
+          if (int r = timed(ctx, PPF_K_SOLVE, [&] {
+                hipLaunchKernelGGL(k_scat_step, dim3(nc), dim3(64), 0, ctx->stream, fa, part,
+                                   split, init, active);
+              }))
+            return r;
+        }
         if (it % kCheck != kCheck - 1 && it <= 1001) continue;
         HIPCHK(ctx, hipMemcpyAsync(ctx->active_h, active, sizeof(int), hipMemcpyDeviceToHost,
                                    ctx->stream));
