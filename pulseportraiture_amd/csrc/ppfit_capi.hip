@@ -149,12 +149,13 @@ void launch_fit_taylor(dim3 g, size_t lds, hipStream_t st, const FitArgs& fa) {
 
 // split scattering solve: below this many running subints the sweeps take
 // one 8-channel group per wave (A/B knob PPF_SCAT_TAIL; 0 keeps the split)
-// the split scattering solve's iterations as hipGraph launches: opt-in
-// (PPF_SCAT_GRAPH=1) until measured; default one launch per kernel
+// the split scattering solve's iterations as hipGraph launches (config 3:
+// 21.95-22.00 -> 21.65-21.67 ms per step, results bitwise the same);
+// PPF_SCAT_GRAPH=0: one launch per kernel (A/B)
 bool scat_graph() {
   static const bool on = [] {
     const char* e = getenv("PPF_SCAT_GRAPH");
-    return e && atoi(e) != 0;
+    return !(e && atoi(e) == 0);
   }();
   return on;
 }
