@@ -110,7 +110,86 @@ def parse():
     ap.add_argument("--host-stream", type=int, default=None,
                     help="also time host-resident (pinned) input streamed over PCIe in chunks "
                          "of this many subints (default: on for config gm; 0: off)")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="libppfit launch-schedule option (ppf_set_option, _lib.OPTIONS); "
+                         "no option changes a result")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check without a GPU: every rank runs the timing and "
+                         "reduction code around a no-op step over gloo (tests only; the line "
+                         "says so and is not a measurement)")
     return ap.parse_args()
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args):
+    """--gpus N > 1 outside a torch.distributed launch: start N ranks of this
+    same command through torch.distributed.run (one process per GPU, rank i
+    on device LOCAL_RANK = i) as a child process -- before anything here has
+    touched the GPU -- and return its exit code.  Rank 0 prints the line."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node=%d" % args.gpus, "--master-addr=127.0.0.1",
+           "--master-port=%d" % free_port(), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+def dist_times(elapsed, world, device=None):
+    """(max over ranks, every rank's time) of one timed region."""
+    if world == 1:
+        return elapsed, [elapsed]
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    every = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(every, t)
+    every = [float(x.item()) for x in every]
+    return max(every), every
+
+
+def main_dry_run(args):
+    """--dry-run: the rank / barrier / max-over-ranks / JSON-line path of a
+    multi-rank run without a device (gloo on the CPU), each step a no-op."""
+    import torch.distributed as dist
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    nsub = args.nsub or CONFIGS[args.config][0]
+    for _ in range(args.warmup):
+        pass
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.001)
+    if world > 1:
+        dist.barrier()
+    elapsed, every = dist_times(time.perf_counter() - t0, world)
+    pids = [None] * world
+    if world > 1:
+        dist.all_gather_object(pids, (rank, os.getpid()))
+    else:
+        pids = [(0, os.getpid())]
+    if rank == 0:
+        print(json.dumps({"metric": "dry run (launcher check, no device)", "value": None,
+                          "unit": "TOAs/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+                          "rank_ms_per_step": [t / args.steps * 1e3 for t in every],
+                          "higher_is_better": True, "scaling": "weak", "data": "none (dry run)",
+                          "config": {"workload": args.config, "nsub_per_gpu": nsub,
+                                     "parallelism": "subint-sharded dp%d" % world},
+                          "rank_pids": pids}))
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def host_cores():
@@ -223,6 +302,11 @@ def leg_ppalign(eng, narch, niter, seed):
     port = ppalign.align_archives(names, "bench_pa_guess", fit_dm=True, niter=niter, quiet=True)
     torch.cuda.synchronize()
     t = time.perf_counter() - t0
+    # the same call again with a synchronisation at every phase boundary
+    # (diagnostic split of the time above; not the timed call)
+    phases = {}
+    ppalign.align_archives(names, "bench_pa_guess", fit_dm=True, niter=niter, quiet=True,
+                           timings=phases)
     for nm in names + ["bench_pa_guess"]:
         archive.unregister_archive(nm)
     del data
@@ -231,6 +315,7 @@ def leg_ppalign(eng, narch, niter, seed):
             "ms_per_iteration": round(t / niter * 1e3, 2),
             "data_gb": round(narch * nchan * nbin * 8 / 1e9, 2),
             "template_finite": bool(np.isfinite(port).all()),
+            "phase_s": {k: round(v, 4) for k, v in phases.items() if k != "start"},
             "workload": "config 5: %d archives x 1 subint x %d chan x %d bin, fit_dm, niter %d; "
                         "setup (registration, unit stack) inside the timed call"
                         % (narch, nchan, nbin, niter)}
@@ -286,6 +371,10 @@ def cpu_baseline(args, config, data, w, flags, log10_tau, tau_g, host, S):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    if args.dry_run:
+        return main_dry_run(args)
     import torch
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -306,6 +395,9 @@ def main():
                            "ppalign": 0}[config]
     eng = Engine(local if world > 1 else 0)
     E._engines[eng.device.index] = eng  # the drivers' get_engine() uses this context
+    for o in args.opt:
+        k, v = o.split("=")
+        eng.set_option(k, int(v))
 
     if config == "ppalign":
         return main_ppalign(args, eng, rank, world)
@@ -346,11 +438,7 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=eng.device)
-        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed, rank_times = dist_times(t1 - t0, world, eng.device)
     ms_step = elapsed / args.steps * 1e3
     toas = nsub * world * args.steps
     value = toas / elapsed
@@ -421,8 +509,9 @@ def main():
         "metric": "TOAs/sec (phase+DM fit, 64ch×2048bin fp64) at 1/2/4/8 MI355X"
         if config == "headline" else "TOAs/sec (%s)" % config,
         "value": round(value, 2), "unit": "TOAs/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
+        "rank_ms_per_step": [round(t / args.steps * 1e3, 3) for t in rank_times],
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (example.gmodel template, injected phi/DM, sigma=1.5 Philox "
                 "noise; generated on device)",
         "config": {"workload": desc, "nsub_per_gpu": nsub, "nchan": nchan, "nbin": nbin,

@@ -21,6 +21,8 @@
  *   ppf_unpack_subints      <- PSRCHIVE Archive_load + pscrunch in
  *                              pplib.load_data  pplib.py:2670-2732 (with
  *                              include/ppfits.h, the host PSRFITS reader)
+ *   ppf_profile_snr         <- Profile::snr() for load_data's SNRs
+ *                              pplib.py:2762-2770 (PSRCHIVE restated)
  *   ppf_gaussian_portraits  <- pplib.gen_gaussian_portrait / read_model
  *                              pplib.py:853-930, 2873-2959
  *   ppf_scatter_rotate_rows <- GetTOAs.show_fit port/model  pptoas.py:1389-1402
@@ -91,17 +93,44 @@ int ppf_synchronize(ppf_ctx* ctx);
  * into `pieces` launches alternating between the context stream and a
  * second internal queue, piece p's data pass ordered after piece p-1's, so
  * one piece's latency-bound solver kernels overlap the next one's HBM-bound
- * pass.  Results are bitwise those of pieces = 1.  0 = default (PPF_PIPE
- * environment variable, else the library default); at most 64.            */
+ * pass.  Results are bitwise those of pieces = 1.  0 = the library default
+ * (1: measured no faster); at most 64.                        */
 int ppf_set_pipeline(ppf_ctx* ctx, int32_t pieces);
+/* Launch-schedule options of one context (diagnostic / A-B use; the
+ * library reads no environment variables).  None of them changes a
+ * result: every setting gives bitwise the same fits (tests/test_gpu_options.py).
+ *   PPF_OPT_SCAT_GRAPH   1: the split scattering solve launches each group of
+ *                        four iterations as one hipGraph (default); 0: one
+ *                        launch per kernel.
+ *   PPF_OPT_SCAT_SPLIT   1: trust-ncg scattering fits spread every evaluation
+ *                        over several workgroups (k_scat_sweep/k_scat_step,
+ *                        default); 0: one workgroup per subint (k_solve).
+ *   PPF_OPT_SCAT_TAIL    running subints below which the split solve takes
+ *                        one 8-channel group per wave (default 512; 0 never).
+ *   PPF_OPT_FUSE_MOMENTS 1: the first Taylor moment pass runs inside
+ *                        k_fit_taylor (default); 0: its own k_moments launch.
+ *   PPF_OPT_GUESS_WAVE   1: the single-wave guess kernel takes the subints it
+ *                        covers (default); 0: every guess in k_guess.       */
+#define PPF_OPT_SCAT_GRAPH 0
+#define PPF_OPT_SCAT_SPLIT 1
+#define PPF_OPT_SCAT_TAIL 2
+#define PPF_OPT_FUSE_MOMENTS 3
+#define PPF_OPT_GUESS_WAVE 4
+#define PPF_NUM_OPTS 5
+int ppf_set_option(ppf_ctx* ctx, int32_t option, int32_t value);
+int ppf_get_option(const ppf_ctx* ctx, int32_t option, int32_t* value);
 /* Upper bound on workspace bytes the context may hold (default 32 GiB). */
 int ppf_set_workspace_limit(ppf_ctx* ctx, int64_t bytes);
 /* Per-kernel HIP-event timing on the context stream (off by default). */
 int ppf_set_timing(ppf_ctx* ctx, int enable);
 /* Diagnostic: record every objective sweep of the TNC and Newton-CG solvers
- * (the point, f, gradient, Hessian terms, whether it counts in nfev) into
- * buf [nsub][cap][32] doubles (device memory, caller-owned; batch subint
- * index), at most cap sweeps per subint.  cap 0 turns it off.             */
+ * and of the split trust-ncg scattering solve (the point, f, gradient,
+ * Hessian terms, whether it counts in nfev) into buf [nsub][cap][32]
+ * doubles (device memory, caller-owned; batch subint index), at most cap
+ * sweeps per subint.  cap 0 turns it off.  Split scattering records also
+ * hold, in fields 28-31, the trust radius after the evaluation's update,
+ * the predicted reduction and rho of the step that led to it, and its
+ * Steihaug boundary flag.                                                 */
 int ppf_set_trace(ppf_ctx* ctx, double* buf, int32_t cap);
 int ppf_get_kernel_time(ppf_ctx* ctx, int kernel_id, double* total_ms,
                         int64_t* launches);
@@ -293,6 +322,24 @@ int ppf_unpack_subints(ppf_ctx* ctx, int32_t nsub, int32_t npol, int32_t nchan, 
 int ppf_remove_baseline(ppf_ctx* ctx, int32_t nsub, int32_t npol, int32_t nchan, int32_t nbin,
                         int32_t ntot, int32_t width, double* data, const double* weights,
                         int32_t* window);
+
+/* Per-profile S/N, load_data's SNRs[isub, ipol, ichan] =
+ * Profile::snr() (pplib.py:2762-2770; get_TOAs weights guess_fit_freq with
+ * them, pptoas.py:401).  Restated from PSRCHIVE's default "phase" S/N
+ * estimator (PSRCHIVE is not in this image: PARITY UNPINNED):
+ *   off-pulse window: the circular run of `width` bins with the smallest
+ *     sum (first on ties; windows summed bin by bin from their start);
+ *   m, v: mean and sample variance (n - 1) over that window;
+ *   edges (cumulative-power peak): with y the profile minus m read
+ *     circularly from the bin after the window, c its running sum and
+ *     C = c[nbin - 1], rise = the first bin with c >= threshold C, fall =
+ *     the first with c >= (1 - threshold) C;
+ *   snr = (c[fall] - c[rise] + y[rise]) / sqrt(fall - rise + 1) / sqrt(v),
+ *     0 when C <= 0 or v <= 0.
+ * rows [nrow][nbin] (nbin <= 8192), out [nrow].  Callers pass width =
+ * floor(0.15 nbin) and threshold 0.1.                                      */
+int ppf_profile_snr(ppf_ctx* ctx, int32_t nrow, int32_t nbin, const double* rows, int32_t width,
+                    double threshold, double* out);
 
 /* out[r] = irfft(rfft(in[r]) e^{2 pi i k phase[r]} / (1 + 2 pi i k tau[r]))
  * (rotate_portrait_full of a scattered template, pptoas.py:1389-1397);

@@ -135,6 +135,65 @@ def remove_baseline(subints, weights, ntot=1, duty=0.15):
     return d, starts
 
 
+def profile_snr(rows, duty=0.15, threshold=0.1):
+    """Profile::snr() as load_data fills SNRs (pplib.py:2762-2770), restated
+    from PSRCHIVE's default "phase" S/N estimator: off-pulse window = the
+    circular run of floor(duty nbin) bins of smallest sum (first on ties),
+    its mean m and sample variance v; the on-pulse edges from the running
+    power of y = row - m read from the bin after the window (the first bins
+    where it reaches threshold and 1 - threshold of the total C); snr =
+    sum(y[rise..fall]) / sqrt(fall - rise + 1) / sqrt(v) (0 if C <= 0 or
+    v <= 0).  PARITY UNPINNED: PSRCHIVE is not in this image and the
+    reference ships no archives.  The sums run in the order ppf_profile_snr
+    forms them (window sums bin by bin from the start; the running power in
+    64 contiguous segments, then the segment totals in order), so discrete
+    choices (window, edges) are the device's on the same rows."""
+    x = np.atleast_2d(np.asarray(rows, dtype=float))
+    shape = np.shape(rows)[:-1]
+    nrow, nbin = x.shape
+    width = max(1, int(duty * nbin))
+    out = np.zeros(nrow)
+    per = (nbin + 63) // 64
+    for r in range(nrow):
+        row = x[r]
+        box = np.zeros(nbin)
+        for i in range(width):  # sequential per window start, as the device
+            box = box + row[(np.arange(nbin) + i) % nbin]
+        j0 = int(np.argmin(box))
+        win = row[(j0 + np.arange(width)) % nbin]
+        m = 0.0
+        for v_ in win:
+            m += v_
+        m /= width
+        v = 0.0
+        for v_ in win:
+            v += (v_ - m) * (v_ - m)
+        v = v / (width - 1) if width > 1 else 0.0
+        y = row[(j0 + width + np.arange(nbin)) % nbin] - m
+        segs = [(min(nbin, q * per), min(nbin, q * per + per)) for q in range(64)]
+        tot = []
+        for i0, i1 in segs:  # each segment summed in sequence
+            t = 0.0
+            for i in range(i0, i1):
+                t += y[i]
+            tot.append(t)
+        pre, C = [], 0.0
+        for t in tot:  # exclusive prefix of the totals, in order
+            pre.append(C)
+            C += t
+        rise = fall = None
+        for (i0, i1), cc in zip(segs, pre):
+            for i in range(i0, i1):
+                cc += y[i]
+                if rise is None and cc >= threshold * C:
+                    rise, crise, yrise = i, cc, y[i]
+                if fall is None and cc >= (1.0 - threshold) * C:
+                    fall, cfall = i, cc
+        if C > 0 and v > 0 and rise is not None and fall is not None and fall >= rise:
+            out[r] = (cfall - crise + yrise) / np.sqrt(fall - rise + 1) / np.sqrt(v)
+    return out.reshape(shape)
+
+
 def phase_shifts(phi, DM, GM, freqs, nu_DM=np.inf, nu_GM=np.inf, P=None):
     """Per-channel delay [rot], pptoaslib.py:181-214 (mod=False)."""
     if P is None:

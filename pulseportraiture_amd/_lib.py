@@ -24,6 +24,8 @@ PPF_SOLVE_EXACT = 1
 PPF_SOLVE_EVAL = 2
 PPF_GUESS_DIRECT = 4
 PPF_SELFTEST_N = 10
+# ppf_set_option ids (include/ppfit.h)
+OPTIONS = {"scat_graph": 0, "scat_split": 1, "scat_tail": 2, "fuse_moments": 3, "guess_wave": 4}
 PPF_PHASE_N = 32
 
 _dp = ctypes.c_void_p  # device pointers travel as plain addresses
@@ -66,6 +68,9 @@ EXPORTS = {
     "ppf_set_workspace_limit": ([ctypes.c_void_p, ctypes.c_int64], ctypes.c_int),
     "ppf_set_timing": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
     "ppf_set_trace": ([ctypes.c_void_p, _dp, ctypes.c_int32], ctypes.c_int),
+    "ppf_set_option": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32], ctypes.c_int),
+    "ppf_get_option": ([ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)],
+                       ctypes.c_int),
     "ppf_get_kernel_time": ([ctypes.c_void_p, ctypes.c_int,
                              ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(ctypes.c_int64)], ctypes.c_int),
@@ -108,6 +113,8 @@ EXPORTS = {
     "ppf_remove_baseline": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                              ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _dp, _dp, _dp],
                             ctypes.c_int),
+    "ppf_profile_snr": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, _dp, ctypes.c_int32,
+                         ctypes.c_double, _dp], ctypes.c_int),
     "ppf_synth_portraits": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
                              ctypes.c_int32, _dp, _dp, ctypes.c_double,
                              ctypes.c_uint64, ctypes.c_int64, _dp], ctypes.c_int),

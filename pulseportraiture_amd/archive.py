@@ -127,6 +127,8 @@ def normalize(b, name="archive", subints=True):
 # sources: metadata + a reader of raw subint ranges
 # ---------------------------------------------------------------------------
 class _Registered:
+    owns_reads = False  # read() returns views of the caller's registered array
+
     def __init__(self, name):
         self.base = _registry[name]
 
@@ -136,11 +138,44 @@ class _Registered:
     def read(self, lo, hi):
         return self.base.subints[lo:hi]
 
+    def close(self):
+        pass
+
+
+def _npy_member(path, member):
+    """(dtype, shape, fortran_order, data offset or None) of an .npz member
+    from its .npy header alone.  The offset is the member's array data in the
+    .npz file itself when the member is stored uncompressed (np.savez), so
+    subint ranges can be memory-mapped; None for a compressed member."""
+    import zipfile
+    with zipfile.ZipFile(path) as zf:
+        info = zf.getinfo(member)
+        with zf.open(info) as f:
+            ver = np.lib.format.read_magic(f)
+            rd = np.lib.format.read_array_header_1_0 if ver == (1, 0) else \
+                np.lib.format.read_array_header_2_0
+            shape, fortran, dtype = rd(f)
+            hdr = f.tell()
+    off = None
+    if info.compress_type == zipfile.ZIP_STORED:
+        with open(path, "rb") as raw:
+            raw.seek(info.header_offset)
+            lh = raw.read(30)  # local file header: name / extra lengths at 26 / 28
+            n, m = int.from_bytes(lh[26:28], "little"), int.from_bytes(lh[28:30], "little")
+            off = info.header_offset + 30 + n + m + hdr
+    return dtype, tuple(shape), fortran, off
+
 
 class _Npz:
+    """An .npz archive (save_archive).  The metadata comes from the small
+    members and the subints' .npy header (no DATA read); read(lo, hi) maps
+    only rows lo:hi of a stored member (a compressed one is loaded once)."""
+    owns_reads = True
+
     def __init__(self, path):
         self.z = np.load(path, allow_pickle=False)
         self.path = path
+        self._full = None
 
     def meta(self):
         z = self.z
@@ -153,14 +188,26 @@ class _Npz:
                 b[k[5:]] = v.item() if v.ndim == 0 else v
         if "dmc" in b:
             b["dmc"] = int(b["dmc"])
-        sh = z["subints"].shape  # a .npy header read; the data load is in read()
+        _, sh, _, _ = _npy_member(self.path, "subints.npy")
         sh = sh if len(sh) == 4 else (sh[0], 1) + tuple(sh[1:])
         b.update(nsub=sh[0], npol=sh[1], nchan=sh[2], nbin=sh[3])
         return normalize(b, self.path, subints=False)
 
     def read(self, lo, hi):
-        s = self.z["subints"]
-        return (s if s.ndim == 4 else s[:, None])[lo:hi]
+        dtype, sh, fortran, off = _npy_member(self.path, "subints.npy")
+        if off is not None and not fortran:
+            mm = np.memmap(self.path, dtype=dtype, mode="r", offset=off, shape=sh)
+            s = np.array(mm[lo:hi])  # only these rows are read
+            del mm
+        else:
+            if self._full is None:
+                self._full = self.z["subints"]
+            s = self._full[lo:hi]
+        return s if s.ndim == 4 else s[:, None]
+
+    def close(self):
+        self._full = None
+        self.z.close()
 
 
 def _source(filename, pscrunch):
@@ -219,12 +266,23 @@ class Archive:
     """An opened archive: ``meta`` holds every load_data key but ``subints``
     (after the requested processing); ``read(lo, hi)`` returns processed
     subints [hi - lo, npol, nchan, nbin] -- a numpy array when nothing had to
-    run on the device, else a float64 device tensor."""
+    run on the device, else a float64 device tensor.
+
+    An Archive holds no open file: the source is opened for the metadata
+    and closed again, and every read() reopens it for just that range, so a
+    driver may keep one Archive per datafile for any number of datafiles."""
 
     def __init__(self, filename, dedisperse=False, dededisperse=False, tscrunch=False,
                  pscrunch=False, rm_baseline=True, quiet=True):
-        self.src = _source(filename, pscrunch)
-        raw = self.src.meta()
+        self._src_args = (filename, pscrunch)
+        src = _source(filename, pscrunch)
+        try:
+            raw = src.meta()
+            period_at = getattr(src, "period_at", None)
+            self.eager_noise = bool(getattr(src, "eager_noise", False))
+            self.owns_reads = bool(getattr(src, "owns_reads", True))
+        finally:
+            src.close()
         if not isinstance(filename, str):
             filename = raw.get("filename", "archive")
         raw.setdefault("filename", filename)
@@ -241,7 +299,7 @@ class Archive:
         m.dmc = dmc
         m.baseline_removed = bool(raw.get("baseline_removed", True) or rm_baseline)
         if self.tscrunch:
-            m = _tscrunch_meta(m, getattr(self.src, "period_at", None))
+            m = _tscrunch_meta(m, period_at)
         self.meta = m
         if not quiet:
             print("\nReading data from %s on source %s..." % (filename, m.get("source", "")))
@@ -249,6 +307,13 @@ class Archive:
     @property
     def nsub(self):
         return self.meta.nsub
+
+    def _read_src(self, lo, hi):
+        src = _source(*self._src_args)
+        try:
+            return src.read(lo, hi)
+        finally:
+            src.close()
 
     def _process(self, sub, lo, hi):
         """dedisperse / dededisperse, then remove_baseline, on subints lo:hi."""
@@ -260,7 +325,7 @@ class Archive:
         r = self.raw
         if _is_tensor(sub) and sub.device == eng.device:
             d = sub.to(torch.float64).contiguous()
-            if d.data_ptr() == sub.data_ptr():
+            if not self.owns_reads and d.data_ptr() == sub.data_ptr():
                 d = d.clone()  # never modify a caller's registered tensor
         else:
             d = torch.as_tensor(np.ascontiguousarray(sub, dtype=np.float64), device=eng.device)
@@ -273,15 +338,25 @@ class Archive:
             eng.remove_baseline(d, r.weights[lo:hi], ntot=ntot, duty=DUTY_CYCLE)
         return d
 
+    @staticmethod
+    def snrs(sub):
+        """load_data's SNRs of processed subints [n, npol, nchan, nbin]
+        (Profile::snr() per profile, pplib.py:2762-2770; ppf_profile_snr,
+        PSRCHIVE's default estimator restated, parity unpinned) as numpy
+        [n, npol, nchan].  Sources with snr_deferred metadata (PSRFITS) fill
+        SNRs this way from the data they read."""
+        from .engine import get_engine
+        return get_engine().profile_snr(sub).cpu().numpy()
+
     def read(self, lo=0, hi=None):
         if self.tscrunch:  # the one averaged subint needs every raw subint
             from .engine import get_engine
             r = self.raw
-            sub = self._process(self.src.read(0, r.nsub), 0, r.nsub)
+            sub = self._process(self._read_src(0, r.nsub), 0, r.nsub)
             out, _ = get_engine().tscrunch(sub, r.weights)
             return out
         hi = self.meta.nsub if hi is None else hi
-        return self._process(self.src.read(lo, hi), lo, hi)
+        return self._process(self._read_src(lo, hi), lo, hi)
 
 
 def open_archive(filename, dedisperse=False, dededisperse=False, tscrunch=False, pscrunch=False,
@@ -313,11 +388,17 @@ def load_data(filename, state=None, dedisperse=False, dededisperse=False, tscrun
                      tscrunch=tscrunch, pscrunch=pscrunch, rm_baseline=rm_baseline, quiet=quiet)
     b = DataBunch(**dict(a.meta))
     sub = a.read()
-    if b.get("noise_stds") is None and getattr(a.src, "eager_noise", False):
+    if b.get("noise_stds") is None and a.eager_noise:
         from .engine import get_engine
         n, npol, nchan, nbin = tuple(sub.shape)
         b.noise_stds = get_engine().noise_rows(sub.reshape(-1, nbin)).reshape(
             n, npol, nchan).cpu().numpy()
+    if b.get("snr_deferred"):
+        if get_SNRs:
+            b.SNRs = a.snrs(sub)
+        else:
+            b.SNRs = np.zeros_like(np.asarray(b.SNRs))  # pplib.py:2762 (get_SNRs=False)
+        b.snr_deferred = False
     b.subints = host_array(sub) if host else sub
     for k in ("ok_isubs", "ok_ichans", "masks"):
         b.pop(k, None)

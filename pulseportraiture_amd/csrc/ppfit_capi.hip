@@ -54,6 +54,8 @@ struct ppf_ctx {
   std::vector<hipEvent_t> pool;
   double* trace = nullptr;  // solver trace buffer (ppf_set_trace), device
   int trace_cap = 0;
+  // launch-schedule options (ppf_set_option; include/ppfit.h)
+  int opt[PPF_NUM_OPTS] = {1, 1, 512, 1, 1};
   double ktime[PPF_NUM_KERNELS] = {0};
   int64_t klaunch[PPF_NUM_KERNELS] = {0};
 };
@@ -123,50 +125,7 @@ int twiddles(ppf_ctx* ctx, int nbin, const double2** out) {
   return PPF_OK;
 }
 
-int moments_u() {
-  static const int u = [] {
-    const char* e = getenv("PPF_MOMENTS_U");
-    return (e && atoi(e) == 8) ? 8 : 4;
-  }();
-  return u;
-}
-
-// first moment pass inside k_fit_taylor (default) or its own k_moments
-// launch (A/B knob PPF_FUSE_MOMENTS=0)
-bool fuse_moments() {
-  static const bool f = [] {
-    const char* e = getenv("PPF_FUSE_MOMENTS");
-    return !(e && atoi(e) == 0);
-  }();
-  return f;
-}
-void launch_fit_taylor(dim3 g, size_t lds, hipStream_t st, const FitArgs& fa) {
-  if (fuse_moments())
-    hipLaunchKernelGGL(k_fit_taylor<true>, g, dim3(kBlock), lds, st, fa);
-  else
-    hipLaunchKernelGGL(k_fit_taylor<false>, g, dim3(kBlock), lds, st, fa);
-}
-
-// split scattering solve: below this many running subints the sweeps take
-// one 8-channel group per wave (A/B knob PPF_SCAT_TAIL; 0 keeps the split)
-// the split scattering solve's iterations as hipGraph launches (config 3:
-// 21.95-22.00 -> 21.65-21.67 ms per step, results bitwise the same);
-// PPF_SCAT_GRAPH=0: one launch per kernel (A/B)
-bool scat_graph() {
-  static const bool on = [] {
-    const char* e = getenv("PPF_SCAT_GRAPH");
-    return !(e && atoi(e) == 0);
-  }();
-  return on;
-}
-
-int scat_tail_subints() {
-  static const int v = [] {
-    const char* e = getenv("PPF_SCAT_TAIL");
-    return e ? atoi(e) : 512;
-  }();
-  return v;
-}
+void launch_fit_taylor(const ppf_ctx* ctx, dim3 g, size_t lds, hipStream_t st, const FitArgs& fa);
 
 int vpow_table(ppf_ctx* ctx, int nbin, const double2** out) {
   const int l = ilog2_exact(nbin);
@@ -227,27 +186,6 @@ int sync_event(ppf_ctx* ctx, size_t i, hipEvent_t* out) {
   return PPF_OK;
 }
 
-// the single-wave guess (k_guess_w) for the subints it covers; PPF_GUESS_WAVE=0
-// leaves every guess to k_guess (A/B timing)
-bool guess_wave_on() {
-  static const bool on = [] {
-    const char* e = getenv("PPF_GUESS_WAVE");
-    return !(e && atoi(e) == 0);
-  }();
-  return on;
-}
-
-// default pieces per chunk of the two-queue pipeline on the Taylor path
-// (PPF_PIPE overrides; 1 = one queue, the chunk as one launch per kernel)
-int pipe_default() {
-  static const int n = [] {
-    const char* e = getenv("PPF_PIPE");
-    const int v = e ? atoi(e) : 1;
-    return std::max(1, std::min(64, v));
-  }();
-  return n;
-}
-
 int resolve_timing(ppf_ctx* ctx) {
   for (auto& t : ctx->pending) {
     HIPCHK(ctx, hipEventSynchronize(t.b));
@@ -300,6 +238,15 @@ int model_spectra(ppf_ctx* ctx, int nrow, int nbin, const double* model, int zer
 }
 
 size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+// the first moment pass inside k_fit_taylor (default) or its own k_moments
+// launch (PPF_OPT_FUSE_MOMENTS = 0)
+void launch_fit_taylor(const ppf_ctx* ctx, dim3 g, size_t lds, hipStream_t st, const FitArgs& fa) {
+  if (ctx->opt[PPF_OPT_FUSE_MOMENTS])
+    hipLaunchKernelGGL(k_fit_taylor<true>, g, dim3(kBlock), lds, st, fa);
+  else
+    hipLaunchKernelGGL(k_fit_taylor<false>, g, dim3(kBlock), lds, st, fa);
+}
 
 }  // namespace
 
@@ -355,6 +302,22 @@ int ppf_set_stream(ppf_ctx* ctx, void* stream) {
 int ppf_set_pipeline(ppf_ctx* ctx, int32_t pieces) {
   if (!ctx || pieces < 0 || pieces > 64) return PPF_ERR_INVALID;
   ctx->pipe = pieces;
+  return PPF_OK;
+}
+
+int ppf_set_option(ppf_ctx* ctx, int32_t option, int32_t value) {
+  if (!ctx) return PPF_ERR_INVALID;
+  if (option < 0 || option >= PPF_NUM_OPTS)
+    return fail(ctx, PPF_ERR_INVALID, "unknown option %d", option);
+  if (option == PPF_OPT_SCAT_TAIL ? value < 0 : (value != 0 && value != 1))
+    return fail(ctx, PPF_ERR_INVALID, "option %d: bad value %d", option, value);
+  ctx->opt[option] = value;
+  return PPF_OK;
+}
+
+int ppf_get_option(const ppf_ctx* ctx, int32_t option, int32_t* value) {
+  if (!ctx || !value || option < 0 || option >= PPF_NUM_OPTS) return PPF_ERR_INVALID;
+  *value = ctx->opt[option];
   return PPF_OK;
 }
 
@@ -516,7 +479,7 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   fa.guess_wrap = d->guess_wrap;
   fa.solver_flags = d->solver_flags;
   fa.method = d->method;
-  fa.guess_wave = guess_wave_on() ? 1 : 0;
+  fa.guess_wave = ctx->opt[PPF_OPT_GUESS_WAVE];
   for (int i = 0; i < 5; ++i)
     for (int j = 0; j < 2; ++j) fa.bounds[i][j] = d->bounds ? d->bounds[2 * i + j] : NAN;
   fa.X = sa.X;
@@ -572,11 +535,9 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   const size_t lds_taylor = lds_meta + (fa.tlds ? tl_bytes : 0);
   // trust-ncg scattering fits: every evaluation split over blocks of >= 64
   // fitted channels (k_scat_sweep / k_scat_step)
-  static const bool split_on = [] {
-    const char* e = getenv("PPF_SCAT_SPLIT");  // 0: one block per subint (k_solve<true>)
-    return !(e && atoi(e) == 0);
-  }();
-  const bool split_scat = split_on && d->fit_flags[3] && d->method == PPF_METHOD_TRUST_NCG;
+  // (PPF_OPT_SCAT_SPLIT = 0: one block per subint, k_solve<true>)
+  const bool split_scat = ctx->opt[PPF_OPT_SCAT_SPLIT] && d->fit_flags[3] &&
+                          d->method == PPF_METHOD_TRUST_NCG;
   const int split = std::max(1, std::min(16, nchan / 64));
   if (split_scat) {
     if (int r = ensure(ctx, ctx->spart,
@@ -589,7 +550,7 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   // p's data pass starts when piece p-1's has finished, so the latency-bound
   // guess / fit / post-fit kernels of one piece run beside the HBM-bound
   // data pass of the next.  Each piece owns its slice of the workspace.
-  const int pieces = ctx->pipe > 0 ? ctx->pipe : pipe_default();
+  const int pieces = ctx->pipe > 0 ? ctx->pipe : 1;
   const bool phase_family = !d->fit_flags[3] && !d->fit_flags[4];
   if (taylor && !tnc && phase_family && pieces > 1) {
     if (!ctx->stream2)
@@ -636,17 +597,14 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
               hipLaunchKernelGGL(k_guess, dim3(n), dim3(kBlock), d->guess ? lds_guess : 0, st, fp);
             }))
           return r;
-        if (!fuse_moments())
+        if (!ctx->opt[PPF_OPT_FUSE_MOMENTS])
           if (int r = timed_on(ctx, PPF_K_MOMENTS, st, [&] {
                 const dim3 g(n, (nchan + 16 * kWaves - 1) / (16 * kWaves));
-                if (moments_u() == 4)
-                  hipLaunchKernelGGL(k_moments<4>, g, dim3(kBlock), 0, st, fp);
-                else
-                  hipLaunchKernelGGL(k_moments<8>, g, dim3(kBlock), 0, st, fp);
+                hipLaunchKernelGGL(k_moments<4>, g, dim3(kBlock), 0, st, fp);
               }))
             return r;
         if (int r = timed_on(ctx, PPF_K_FIT_TAYLOR, st, [&] {
-              launch_fit_taylor(dim3(n), lds_taylor, st, fp);
+              launch_fit_taylor(ctx, dim3(n), lds_taylor, st, fp);
             }))
           return r;
         if (int r = timed_on(ctx, PPF_K_POST, st, [&] {
@@ -736,15 +694,20 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
           return fail(ctx, PPF_ERR_DEVICE, "scattering solve graph: %s", hipGetErrorString(e));
         return PPF_OK;
       };
+      // the execs are destroyed on every way out of the loop, error returns
+      // included, after the work launched from them has drained
       struct GraphFree {
         hipGraphExec_t* g;
+        hipStream_t st;
         ~GraphFree() {
+          if (!g[0] && !g[1]) return;
+          (void)hipStreamSynchronize(st);
           for (int i = 0; i < 2; ++i)
             if (g[i]) (void)hipGraphExecDestroy(g[i]);
         }
-      } gfree{gx};
+      } gfree{gx, ctx->stream};
       for (int it = 0, init = 1;; ++it, init = 0) {
-        if (scat_graph() && it >= kCheck && it % kCheck == 0 && it + kCheck - 1 <= 1001) {
+        if (ctx->opt[PPF_OPT_SCAT_GRAPH] && it >= kCheck && it % kCheck == 0 && it + kCheck - 1 <= 1001) {
           hipGraphExec_t* ex = &gx[cur == split ? 0 : 1];
           if (int r = graph_for(cur, ex)) return r;
           if (int r = timed(ctx, PPF_K_SOLVE, [&] { (void)hipGraphLaunch(*ex, ctx->stream); }))
@@ -768,24 +731,20 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
                                    ctx->stream));
         HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
         if (*ctx->active_h == 0 || it > 1001) break;  // trust-ncg stops at 1000 iterations
-        if (*ctx->active_h < scat_tail_subints()) cur = split_tail;
+        if (*ctx->active_h < ctx->opt[PPF_OPT_SCAT_TAIL]) cur = split_tail;
       }
     }
     if (taylor) {
       // the first moment pass inside k_fit_taylor (default), or its own
-      // launch (PPF_FUSE_MOMENTS=0)
-      if (!fuse_moments())
+      // launch (PPF_OPT_FUSE_MOMENTS = 0)
+      if (!ctx->opt[PPF_OPT_FUSE_MOMENTS])
         if (int r = timed(ctx, PPF_K_MOMENTS, [&] {
               const dim3 g(nc, (nchan + 16 * kWaves - 1) / (16 * kWaves));
-              // steps in flight per wave (tuning knob PPF_MOMENTS_U = 4 / 8)
-              if (moments_u() == 4)
-                hipLaunchKernelGGL(k_moments<4>, g, dim3(kBlock), 0, ctx->stream, fa);
-              else
-                hipLaunchKernelGGL(k_moments<8>, g, dim3(kBlock), 0, ctx->stream, fa);
+              hipLaunchKernelGGL(k_moments<4>, g, dim3(kBlock), 0, ctx->stream, fa);
             }))
           return r;
       if (int r = timed(ctx, PPF_K_FIT_TAYLOR, [&] {
-            launch_fit_taylor(dim3(nc), lds_taylor, ctx->stream, fa);
+            launch_fit_taylor(ctx, dim3(nc), lds_taylor, ctx->stream, fa);
           }))
         return r;
     }
@@ -1225,6 +1184,21 @@ int ppf_remove_baseline(ppf_ctx* ctx, int32_t nsub, int32_t npol, int32_t nchan,
   return timed(ctx, PPF_K_UNPACK, [&] {
     hipLaunchKernelGGL(k_remove_baseline, dim3(nsub), dim3(256), (size_t)nbin * sizeof(double),
                        ctx->stream, data, weights, npol, nchan, nbin, ntot, width, window);
+  });
+}
+
+int ppf_profile_snr(ppf_ctx* ctx, int32_t nrow, int32_t nbin, const double* rows, int32_t width,
+                    double threshold, double* out) {
+  if (!ctx || !rows || !out) return fail(ctx, PPF_ERR_INVALID, "null argument");
+  if (nrow <= 0) return PPF_OK;
+  if (nbin <= 0 || nbin > 8192) return fail(ctx, PPF_ERR_INVALID, "nbin %d", nbin);
+  if (width < 1 || width > nbin) return fail(ctx, PPF_ERR_INVALID, "width %d", width);
+  if (!(threshold >= 0.0 && threshold < 0.5))
+    return fail(ctx, PPF_ERR_INVALID, "threshold %g outside [0, 0.5)", threshold);
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  return timed(ctx, PPF_K_UNPACK, [&] {
+    hipLaunchKernelGGL(k_profile_snr, dim3(nrow), dim3(64), (size_t)nbin * sizeof(double),
+                       ctx->stream, rows, nbin, width, threshold, out);
   });
 }
 

@@ -1599,6 +1599,9 @@ __global__ __launch_bounds__(64) void k_scat_step(FitArgs a, const double* part,
   double f, g, xl, Hrow[5] = {0, 0, 0, 0, 0}, tr, predv, pl;
   int hits, k, status, nfev, slot;
   bool done = false;
+  // solver trace (ppf_set_trace): the point this sweep evaluated, its f, g, H
+  double xev = lane < 5 ? (init ? st.x[lane] : st.xp[lane]) : 0.0;
+  double rho_tr = NAN, pred_tr = NAN;
   if (init) {
     load_fgh(f, g, Hrow);
     xl = lane < 5 ? st.x[lane] : 0.0;
@@ -1629,11 +1632,13 @@ __global__ __launch_bounds__(64) void k_scat_step(FitArgs a, const double* part,
     nfev += 1;
     const double actual = f - fp;
     const double pred = f - predv;
+    pred_tr = pred;
     if (pred <= 0.0) {
       status = 2;
       done = true;
     } else {
       const double rho = actual / pred;
+      rho_tr = rho;
       if (rho < 0.25) tr *= 0.25;
       else if (rho > 0.75 && hits) tr = fmin(2.0 * tr, 1000.0);
       if (rho > 0.15) {
@@ -1646,6 +1651,20 @@ __global__ __launch_bounds__(64) void k_scat_step(FitArgs a, const double* part,
       }
       k += 1;
       if (k >= 1000) { status = 1; done = true; }
+    }
+  }
+  if (a.trace && nok) {
+    double xv[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) xv[i] = __shfl(xev, i);
+    const int isw = nfev - 1;
+    if (lane == 0 && isw < a.trace_cap) {
+      trace_sweep(a, s, isw, xv, out, 21, true);
+      double* r = a.trace + ((size_t)s * a.trace_cap + isw) * kTraceRec;
+      r[28] = tr;  // radius after this evaluation's update
+      r[29] = pred_tr;
+      r[30] = rho_tr;
+      r[31] = (double)hits;  // the Steihaug boundary flag of the step that led here
     }
   }
   if (!done) {  // k_solve's loop head: NaN gradient, else the next proposal

@@ -468,6 +468,7 @@ __global__ void k_unpack(const T* raw, const double* scl, const double* offs, in
                          int nchan, int nbin, int pmode, double* out);
 __global__ void k_remove_baseline(double* data, const double* w, int npol, int nchan, int nbin,
                                   int ntot, int width, int* win_out);
+__global__ void k_profile_snr(const double* rows, int nbin, int width, double thr, double* out);
 __global__ void k_scat_taus(const double* freqs, int n, double tau, double alpha, double nu_ref,
                             double* out);
 __global__ void k_guess(FitArgs a);

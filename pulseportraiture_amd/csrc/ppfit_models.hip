@@ -400,6 +400,115 @@ __global__ __launch_bounds__(256) void k_remove_baseline(double* __restrict__ da
   }
 }
 
+// ---------------------------------------------------------------------------
+// Profile::snr() for load_data's SNRs (pplib.py:2762-2770), PSRCHIVE's default
+// phase S/N restated (include/ppfit.h ppf_profile_snr).  One wave per
+// profile row, the row in LDS.  The window sums, the window statistics and
+// the running sum are each formed in one fixed order: lane-contiguous
+// segments of the circular row summed in sequence, then the lanes' totals
+// in lane order (a serial exclusive scan over 64 values), so the result
+// does not depend on the launch.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_profile_snr(const double* __restrict__ rows, int nbin,
+                                                    int width, double thr,
+                                                    double* __restrict__ out) {
+  extern __shared__ __align__(16) unsigned char dyn[];
+  double* x = reinterpret_cast<double*>(dyn);  // [nbin]
+  __shared__ double seg[64];
+  const int r = blockIdx.x, lane = threadIdx.x;
+  const double* row = rows + (size_t)r * nbin;
+  for (int j = lane; j < nbin; j += 64) x[j] = row[j];
+  __syncthreads();
+  // window of smallest sum (first start on ties)
+  double best = INFINITY;
+  int bj = 0x7fffffff;
+  for (int j = lane; j < nbin; j += 64) {
+    double b = 0.0;
+    int k = j;
+    for (int i = 0; i < width; ++i) {
+      b += x[k];
+      if (++k == nbin) k = 0;
+    }
+    if (b < best || (b == best && j < bj)) { best = b; bj = j; }
+  }
+  for (int o = 32; o >= 1; o >>= 1) {
+    const double ob = __shfl_xor(best, o);
+    const int oj = __shfl_xor(bj, o);
+    if (ob < best || (ob == best && oj < bj)) { best = ob; bj = oj; }
+  }
+  const int j0 = bj;
+  // window mean and sample variance (serial over the window, lane 0's order
+  // is the window's own: one pass for the mean, one for the squares)
+  double m = 0.0, v = 0.0;
+  if (lane == 0) {
+    int k = j0;
+    for (int i = 0; i < width; ++i) {
+      m += x[k];
+      if (++k == nbin) k = 0;
+    }
+    m /= (double)width;
+    k = j0;
+    for (int i = 0; i < width; ++i) {
+      const double d = x[k] - m;
+      v += d * d;
+      if (++k == nbin) k = 0;
+    }
+    v = width > 1 ? v / (double)(width - 1) : 0.0;
+  }
+  m = __shfl(m, 0);
+  v = __shfl(v, 0);
+  // running sum of y = x - m from the bin after the window, in lane segments
+  const int start = (j0 + width) % nbin;
+  const int per = (nbin + 63) / 64;
+  const int i0 = min(nbin, lane * per), i1 = min(nbin, i0 + per);
+  double s = 0.0;
+  for (int i = i0; i < i1; ++i) {
+    int k = start + i;
+    if (k >= nbin) k -= nbin;
+    s += x[k] - m;
+  }
+  seg[lane] = s;
+  __syncthreads();
+  if (lane == 0) {
+    double c = 0.0;
+    for (int q = 0; q < 64; ++q) {
+      const double t = seg[q];
+      seg[q] = c;  // exclusive prefix
+      c += t;
+    }
+    best = c;  // total C on lane 0
+  }
+  __syncthreads();
+  const double C = __shfl(best, 0);
+  // first crossings of thr C and (1 - thr) C: each lane rescans its segment
+  int rise = 0x7fffffff, fall = 0x7fffffff;
+  double crise = 0.0, cfall = 0.0, yrise = 0.0;
+  {
+    double c = seg[lane];
+    for (int i = i0; i < i1; ++i) {
+      int k = start + i;
+      if (k >= nbin) k -= nbin;
+      const double y = x[k] - m;
+      c += y;
+      if (rise == 0x7fffffff && c >= thr * C) { rise = i; crise = c; yrise = y; }
+      if (fall == 0x7fffffff && c >= (1.0 - thr) * C) { fall = i; cfall = c; }
+    }
+  }
+  for (int o = 32; o >= 1; o >>= 1) {
+    const int orise = __shfl_xor(rise, o), ofall = __shfl_xor(fall, o);
+    const double ocr = __shfl_xor(crise, o), oyr = __shfl_xor(yrise, o),
+                 ocf = __shfl_xor(cfall, o);
+    if (orise < rise) { rise = orise; crise = ocr; yrise = oyr; }
+    if (ofall < fall) { fall = ofall; cfall = ocf; }
+  }
+  if (lane == 0) {
+    double snr = 0.0;
+    if (C > 0.0 && v > 0.0 && rise != 0x7fffffff && fall != 0x7fffffff && fall >= rise)
+      snr = (cfall - crise + yrise) / sqrt((double)(fall - rise + 1)) / sqrt(v);
+    out[r] = snr;
+  }
+}
+
 template __global__ void k_unpack<uint8_t>(const uint8_t*, const double*, const double*, int, int,
                                            int, int, int, double*);
 template __global__ void k_unpack<int16_t>(const int16_t*, const double*, const double*, int, int,

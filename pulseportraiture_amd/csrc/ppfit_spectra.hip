@@ -464,10 +464,13 @@ __device__ void c2r_from_spectrum(double2* buf, double2 (&xs)[((1 << LOGN) + kBl
 }
 
 template <int LOGN>
-__global__ __launch_bounds__(kBlock) void k_rotate_rows(const double* __restrict__ in,
+// in == out is supported (ppf_rotate_rows in place, engine.rotate_rows):
+// each workgroup loads its whole row into LDS and synchronises before any
+// store, so in and out are deliberately not __restrict__.
+__global__ __launch_bounds__(kBlock) void k_rotate_rows(const double* in,
                                                         const double* __restrict__ phase,
                                                         const double* __restrict__ tau,
-                                                        double* __restrict__ out,
+                                                        double* out,
                                                         const double2* __restrict__ tw) {
   constexpr int N = 1 << LOGN;
   constexpr int KI = (N + 1 + kBlock - 1) / kBlock;

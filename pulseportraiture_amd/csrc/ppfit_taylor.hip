@@ -291,7 +291,6 @@ __global__ __launch_bounds__(kBlock, 3) void k_moments(FitArgs a) {
 }
 
 template __global__ void k_moments<4>(FitArgs);
-template __global__ void k_moments<8>(FitArgs);
 
 // ---------------------------------------------------------------------------
 // k_fit_taylor: one workgroup per phase-family subint, the whole fit:

@@ -114,12 +114,23 @@ class Engine:
         (ppf_set_pipeline; 0 = library default)."""
         self._chk(self.lib.ppf_set_pipeline(self.ctx, int(pieces)))
 
+    def set_option(self, name, value):
+        """Launch-schedule option of this context (ppf_set_option; names in
+        _lib.OPTIONS).  No setting changes a result."""
+        self._chk(self.lib.ppf_set_option(self.ctx, _lib.OPTIONS[name], int(value)))
+
+    def get_option(self, name):
+        v = ctypes.c_int32()
+        self._chk(self.lib.ppf_get_option(self.ctx, _lib.OPTIONS[name], ctypes.byref(v)))
+        return v.value
+
     def set_timing(self, on=True):
         self._chk(self.lib.ppf_set_timing(self.ctx, int(bool(on))))
 
     def set_trace(self, buf, cap):
-        """Solver trace of the TNC / Newton-CG kernels (ppf_set_trace): buf a
-        float64 device tensor [nsub, cap, 32] or None (off)."""
+        """Solver trace of the TNC / Newton-CG kernels and of the split
+        trust-ncg scattering solve (ppf_set_trace): buf a float64 device
+        tensor [nsub, cap, 32] or None (off)."""
         if buf is None or cap <= 0:
             self._chk(self.lib.ppf_set_trace(self.ctx, None, 0))
             self._trace = None
@@ -508,6 +519,20 @@ class Engine:
                                                _ptr(d), _ptr(w), _ptr(win)))
         win._keep = w
         return win
+
+    def profile_snr(self, rows, duty=0.15, threshold=0.1):
+        """Profile::snr() of every row (ppf_profile_snr, PSRCHIVE's default
+        phase S/N restated; parity unpinned): rows [..., nbin] -> [...]
+        float64 device tensor."""
+        d = _dev_f64(rows, self.device)
+        shape = tuple(d.shape[:-1])
+        nbin = int(d.shape[-1])
+        d = d.reshape(-1, nbin).contiguous()
+        out = torch.empty(d.shape[0], dtype=torch.float64, device=self.device)
+        self._chk(self.lib.ppf_profile_snr(self.ctx, d.shape[0], nbin, _ptr(d),
+                                           max(1, int(duty * nbin)), float(threshold), _ptr(out)))
+        out._keep = d
+        return out.reshape(shape)
 
     def irfft_rows(self, spec, nbin):
         dev = self.device

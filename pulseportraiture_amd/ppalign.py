@@ -128,6 +128,10 @@ class _UnitStack:
             sub = a.read(lo, hi)  # this rank's subint range only
             if not isinstance(sub, torch.Tensor):
                 sub = torch.as_tensor(np.ascontiguousarray(sub), device=dev)
+            snrs = m.SNRs
+            if m.get("snr_deferred"):  # load_data's SNRs of the subints read
+                snrs = np.array(m.SNRs, dtype=np.float64)
+                snrs[lo:hi] = a.snrs(sub)
             ns = m.get("noise_stds")
             for i in idx:
                 _, isub, ichans, mich = units[i]
@@ -151,16 +155,18 @@ class _UnitStack:
                 wts[i, mich] = m.weights[isub, ichans]
                 P[i] = m.Ps[isub]
                 DMg[i] = m.DM
-                nu_fit[i] = guess_fit_freq(m.freqs[isub, ichans], m.SNRs[isub, 0, ichans])
+                nu_fit[i] = guess_fit_freq(m.freqs[isub, ichans], snrs[isub, 0, ichans])
         if need_noise.any():  # load_data's noise_stds (pplib.py:2744-2748), on the device
             noise = eng.noise_rows(self.pols[0].reshape(-1, nbin)).reshape(n, nchan).cpu().numpy()
             errs = np.where(need_noise[:, None] & (mask > 0), noise, errs)
         self.freqs, self.errs, self.mask, self.wts = freqs, errs, mask, wts
         self.P, self.DMg, self.nu_fit = P, DMg, nu_fit
 
-    def fit_and_accumulate(self, eng, model_port, fit_dm, accum, tw):
+    def fit_and_accumulate(self, eng, model_port, fit_dm, accum, tw, mark=None):
         """One iteration's fits (ppalign.py:178-195) and weighted rotate-and-sum
         (ppalign.py:202-208) in the Fourier domain."""
+        import time
+        t0 = time.perf_counter()
         n = self.n
         init = np.stack([np.zeros(n), self.DMg, np.zeros(n), np.zeros(n), np.zeros(n)], 1)
         flags = [1, int(bool(fit_dm)), 0, 0, 0]
@@ -169,6 +175,8 @@ class _UnitStack:
                                   fit_flags=flags, log10_tau=False, chan_mask=self.mask,
                                   weights=self.wts, guess=True, guess_Ns=model_port.shape[1],
                                   guess_wrap=False, guess_nu=self.nu_fit)
+        if mark is not None:
+            t0 = mark("fit", t0)
         phase = res["params"][:, 0]
         DM = res["params"][:, 1]
         nu_ref = res["nu_out"][:, 0]
@@ -179,19 +187,33 @@ class _UnitStack:
         for ipol, pol in enumerate(self.pols):
             eng.rotate_accumulate(pol, ph, w, accum[ipol])
         tw += torch.as_tensor(w.sum(axis=0), device=tw.device)
+        if mark is not None:
+            mark("accumulate", t0)
         return res
 
 
 def align_archives(metafile, initial_guess, fit_dm=True, tscrunch=False, pscrunch=True,
                    SNR_cutoff=0.0, outfile=None, norm=None, rot_phase=0.0, place=None,
-                   niter=1, quiet=False, return_weights=False):
+                   niter=1, quiet=False, return_weights=False, timings=None):
     """Iteratively align and average archives; returns aligned_port[npol, nchan, nbin].
 
     The reference writes the result into a PSRCHIVE archive; here the portrait
     is returned (and written with archive.save_archive when ``outfile`` ends in
-    .npz).
+    .npz).  ``timings`` (diagnostic): a dict that receives the wall time of
+    each phase (open, unit stack, per-iteration fit / accumulate / exchange),
+    with a device synchronisation at every phase boundary.
     """
+    import time
     from .engine import get_engine
+
+    def mark(key, t0):
+        if timings is None:
+            return 0.0
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        timings[key] = timings.get(key, 0.0) + (t - t0)
+        return t
+    t0 = mark("start", 0.0) if timings is not None else 0.0
     if isinstance(metafile, str) and _arch.file_is_type(metafile, "ASCII"):
         datafiles = [ln.strip() for ln in open(metafile).readlines() if ln.strip()]
         if outfile is None:
@@ -211,12 +233,14 @@ def align_archives(metafile, initial_guess, fit_dm=True, tscrunch=False, pscrunc
     skip_these = []
     opened = _open_all(datafiles, model_data, SNR_cutoff, quiet, skip_these, tscrunch, pscrunch)
     units = _units(opened, model_data)
+    t0 = mark("open", t0)
     lo, hi = shard_range(len(units), rank, world)
     mine = units[lo:hi]
     multi = [u for u in mine if len(u[2]) > 1]
     single = [u for u in mine if len(u[2]) <= 1]
     stack = _UnitStack(eng, multi, opened, model_data.freqs[0], npol, nchan, nbin) \
         if multi else None
+    t0 = mark("unit_stack", t0)
     archives = {}
     for name, a in opened:  # 1-channel hack units (rare): their archives on the host
         if any(u[0] == name for u in single):
@@ -232,9 +256,10 @@ def align_archives(metafile, initial_guess, fit_dm=True, tscrunch=False, pscrunc
         accum = torch.zeros(npol, nchan, nharm, 2, dtype=torch.float64, device=dev)
         tw = torch.zeros(nchan, dtype=torch.float64, device=dev)
         if stack is not None:
-            stack.fit_and_accumulate(eng, model_port, fit_dm, accum, tw)
+            stack.fit_and_accumulate(eng, model_port, fit_dm, accum, tw, mark)
         for u in single:  # 1-channel hack, ppalign.py:196-201
             _single_channel(u, archives, model_port, npol, accum, tw, dev)
+        t0 = mark("accumulate", t0 if stack is None else time.perf_counter())
         allreduce_sum(accum, tw)
         spec = torch.view_as_complex(accum).reshape(npol * nchan, nharm)
         port = eng.irfft_rows(spec, nbin).reshape(npol, nchan, nbin)
@@ -242,6 +267,7 @@ def align_archives(metafile, initial_guess, fit_dm=True, tscrunch=False, pscrunc
         port[:, good] = port[:, good] / tw[good][None, :, None]
         aligned = port.cpu().numpy()
         model_port = aligned[0]
+        t0 = mark("exchange", t0)
         niter -= 1
         count += 1
     if norm in ("mean", "max", "prof", "rms", "abs"):

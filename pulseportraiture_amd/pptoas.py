@@ -84,7 +84,18 @@ _LIST_ATTRS = ["obs", "doppler_fs", "nu0s", "nu_fits", "nu_refs", "ok_idatafiles
 
 
 class GetTOAs:
-    """Measure TOAs and DMs from wideband data (pptoas.py:75-738)."""
+    """Measure TOAs and DMs from wideband data (pptoas.py:75-738).
+
+    Under an initialised torch.distributed group the fits are sharded over
+    the ranks (get_TOAs); ``gather_to`` says which ranks then hold the
+    results: "root" (default) -- rank 0 receives every rank's result arrays
+    and assembles all TOAs, the other ranks keep none (write from rank 0);
+    "all" -- every rank assembles the same TOAs.  ``read_bytes_max`` bounds
+    the bytes of one subint-range read of an archive that materialises its
+    data (PSRFITS, .npz): a rank's shard is read and fitted in pieces of at
+    most that size (registered in-memory archives are views, read whole)."""
+    gather_to = "root"
+    read_bytes_max = 8 << 30
 
     def __init__(self, datafiles, modelfile, quiet=False):
         if isinstance(datafiles, (list, tuple)):
@@ -237,7 +248,11 @@ class GetTOAs:
         1329-1344): reloaded with dededisperse=True when dmc = 1."""
         a = self._open(datafile, tscrunch, quiet, rm_base)
         b = DataBunch(**dict(a.meta))
-        b.subints = _arch.host_array(a.read())
+        sub = a.read()
+        if b.get("snr_deferred"):  # load_data's SNRs (pplib.py:2762-2770)
+            b.SNRs = a.snrs(sub)
+            b.snr_deferred = False
+        b.subints = _arch.host_array(sub)
         return b
 
     def get_TOAs(self, datafile=None, tscrunch=False, nu_refs=None, DM0=None, bary=True,
@@ -309,11 +324,19 @@ class GetTOAs:
             t0 = time.time()
             parts[ij] = (a0, self._fit_job(job, a0, a1, fit_scat, method))
             durations[ij] = time.time() - t0
-        # 3. gather every rank's result rows; every rank assembles all TOAs
+        # 3. gather the result arrays: to rank 0 (gather_to "root"), which
+        # assembles every TOA, or to every rank ("all")
         if world > 1:
             import torch.distributed as dist
-            got = [None] * world
-            dist.all_gather_object(got, (parts, durations))
+            if self.gather_to == "all":
+                got = [None] * world
+                dist.all_gather_object(got, (parts, durations))
+            else:
+                got = [None] * world if rank == 0 else None
+                dist.gather_object((parts, durations), got, dst=0)
+                if rank != 0:
+                    self.ok_idatafiles = []  # the results live on rank 0
+                    return
             parts, durations = {}, {}
             for p_r, d_r in got:
                 for ij, v in p_r.items():
@@ -725,10 +748,6 @@ class GetTOAs:
         allok = nchx == nchan
         # reference frequencies (pptoas.py:396-415)
         nu_fits_a = np.zeros((nsub, 3))
-        if nu_fit_tuple is None:
-            nu_fits_a[ok_isubs] = self._guess_fit_freqs(data, ok_isubs, wn, allok)[:, None]
-        else:
-            nu_fits_a[ok_isubs] = [nu_fit_tuple[0], nu_fit_tuple[0], nu_fit_tuple[-1]]
         nu_refs_a = np.full((nsub, 3), np.nan)
         if nu_ref_tuple is not None:
             nu_refs_a[ok_isubs] = [nu_ref_tuple[0], nu_ref_tuple[0], nu_ref_tuple[-1]]
@@ -738,22 +757,8 @@ class GetTOAs:
         init = np.zeros((nsub, 5))
         guess_tau = np.zeros(nsub)
         init[ok_isubs, 1] = DM_stored
-        if fit_scat:
-            P = data.Ps[ok_isubs]
-            nu_fit_tau = nu_fits_a[ok_isubs, 2]
-            if self.scat_guess is not None:
-                ts, tref, alpha_g = self.scat_guess
-                tau_g = (ts / P) * (nu_fit_tau / tref) ** alpha_g
-            else:
-                alpha_g = self.alpha if hasattr(self, "alpha") else scattering_alpha
-                tau_g = (self.gparams[1] / P) * (nu_fit_tau / self.model_nu_ref) ** alpha_g \
-                    if hasattr(self, "gparams") else np.zeros(len(ok_isubs))
-            tau_g = np.asarray(tau_g, dtype=np.float64) * np.ones(len(ok_isubs))
-            guess_tau[ok_isubs] = tau_g
-            if self.log10_tau:
-                tau_g = np.log10(np.where(tau_g == 0.0, nbin ** -1, tau_g))
-            init[ok_isubs, 3] = tau_g
-            init[ok_isubs, 4] = alpha_g
+        self._nu_fit_and_tau(data, ok_isubs, wn, allok, nu_fit_tuple, fit_scat, nu_fits_a, init,
+                             guess_tau)
         # per-subint fit flags (pptoas.py:474-484): get_TOAs keeps one
         # fit_flags list across subints and archives, and a 2-channel subint
         # (fit_DM and fit_GM) zeroes GM in the *previous* subint's list --
@@ -787,7 +792,37 @@ class GetTOAs:
         return DataBunch(name=datafile, data=data, obs=obs, DM0=DM0, MJDs=MJDs, epoch_parts=ep,
                          ok_isubs=ok_isubs, models=models, midx=midx, mask=mask, wn=wn,
                          nchx=nchx, nu_fits_a=nu_fits_a, nu_refs_a=nu_refs_a, init=init,
-                         guess_tau=guess_tau, ff=ff_all, bounds=bounds)
+                         guess_tau=guess_tau, ff=ff_all, bounds=bounds, allok=allok,
+                         nu_fit_tuple=nu_fit_tuple)
+
+    def _nu_fit_and_tau(self, data, isubs, wn, allok, nu_fit_tuple, fit_scat, nu_fits_a, init,
+                        guess_tau):
+        """nu_fit (guess_fit_freq with the channel S/Ns, pptoas.py:396-415)
+        and the scattering guess at nu_fit_tau (pptoas.py:420-440) of subints
+        isubs, into nu_fits_a / init / guess_tau."""
+        if not len(isubs):
+            return
+        nbin = data.nbin
+        if nu_fit_tuple is None:
+            nu_fits_a[isubs] = self._guess_fit_freqs(data, isubs, wn, allok)[:, None]
+        else:
+            nu_fits_a[isubs] = [nu_fit_tuple[0], nu_fit_tuple[0], nu_fit_tuple[-1]]
+        if fit_scat:
+            P = data.Ps[isubs]
+            nu_fit_tau = nu_fits_a[isubs, 2]
+            if self.scat_guess is not None:
+                ts, tref, alpha_g = self.scat_guess
+                tau_g = (ts / P) * (nu_fit_tau / tref) ** alpha_g
+            else:
+                alpha_g = self.alpha if hasattr(self, "alpha") else scattering_alpha
+                tau_g = (self.gparams[1] / P) * (nu_fit_tau / self.model_nu_ref) ** alpha_g \
+                    if hasattr(self, "gparams") else np.zeros(len(isubs))
+            tau_g = np.asarray(tau_g, dtype=np.float64) * np.ones(len(isubs))
+            guess_tau[isubs] = tau_g
+            if self.log10_tau:
+                tau_g = np.log10(np.where(tau_g == 0.0, nbin ** -1, tau_g))
+            init[isubs, 3] = tau_g
+            init[isubs, 4] = alpha_g
 
     @staticmethod
     def _guess_fit_freqs(data, ok_isubs, wn, allok):
@@ -807,14 +842,45 @@ class GetTOAs:
             out[j] = guess_fit_freq(data.freqs[isub, ok], np.asarray(data.SNRs)[isub, 0, ok])
         return out
 
+    def _read_pieces(self, job, subs):
+        """Split subs (ascending subint indices) into runs whose subint range
+        reads at most read_bytes_max bytes (one run for views of registered
+        archives)."""
+        data = job.data
+        if not getattr(job.arch, "owns_reads", True):
+            return [subs]
+        per = 8 * int(data.npol) * int(data.nchan) * int(data.nbin)
+        span = max(1, int(self.read_bytes_max) // per)
+        out, i = [], 0
+        while i < len(subs):
+            j = int(np.searchsorted(subs, subs[i] + span, side="left"))
+            out.append(subs[i:j])
+            i = j
+        return out
+
     def _fit_job(self, job, a0, a1, fit_scat, method):
         """Fit ok subints job.ok_isubs[a0:a1] of one archive: read only their
-        subint range, then one batched device call per flag set.  Returns
-        result rows aligned with job.ok_isubs[a0:a1]."""
-        subs = job.ok_isubs[a0:a1]
+        subint range, in pieces of at most read_bytes_max, then one batched
+        device call per piece and flag set.  Returns result rows aligned with
+        job.ok_isubs[a0:a1]."""
+        pieces = self._read_pieces(job, job.ok_isubs[a0:a1])
+        res = [self._fit_piece(job, p, fit_scat, method) for p in pieces]
+        if len(res) == 1:
+            return res[0]
+        return {k: np.concatenate([r[k] for r in res]) for k in res[0]}
+
+    def _fit_piece(self, job, subs, fit_scat, method):
         data = job.data
         s_lo, s_hi = int(subs[0]), int(subs[-1]) + 1
-        sub = job.arch.read(s_lo, s_hi)[:, 0]  # [s_hi - s_lo, nchan, nbin], numpy or device
+        full = job.arch.read(s_lo, s_hi)  # [s_hi - s_lo, npol, nchan, nbin], numpy or device
+        if data.get("snr_deferred"):
+            # load_data's SNRs (Profile::snr(), pplib.py:2762-2770) of the
+            # subints just read, then their nu_fit and scattering guess
+            from .engine import get_engine
+            data.SNRs[s_lo:s_hi] = get_engine().profile_snr(full).cpu().numpy()
+            self._nu_fit_and_tau(data, subs, job.wn, job.allok, job.nu_fit_tuple, fit_scat,
+                                 job.nu_fits_a, job.init, job.guess_tau)
+        sub = full[:, 0]
         ns = data.get("noise_stds")
         errs = None if ns is None else np.asarray(ns)[:, 0]
         ffs = job.ff[subs]
@@ -840,6 +906,7 @@ class GetTOAs:
                 guess_nu=None, guess_tau=job.guess_tau[s] if fit_scat else None,
                 method=method, bounds=job.bounds)
             keep = {k: np.asarray(res[k]) for k in _RESULT_KEYS if k in res}
+            keep["nu_fit"] = job.nu_fits_a[s]  # the assembling rank's nu_fits
             if len(groups) == 1:
                 return keep
             if out is None:
@@ -980,6 +1047,7 @@ class GetTOAs:
                         data.telescope, data.telescope_code, nuo[:, 0].tolist(),
                         toa_mjds, TOA_err.tolist(), DM.tolist(), DM_err.tolist())
         self.TOA_list.extend(toas)
+        job.nu_fits_a[ok] = res["nu_fit"]  # (computed by whichever rank read the subint)
         nu_fits = list(job.nu_fits_a)  # list(np.zeros([nsub, 3])) filled (pptoas.py:283,406)
         nr = np.zeros((nsub, 3))  # pptoas.py:284, ok rows from the fit (:527-530)
         nr[ok] = nuo

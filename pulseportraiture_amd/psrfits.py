@@ -185,6 +185,7 @@ class PSRFITSSource:
     (ppfits_read_raw) and unpacked + pscrunched on the device
     (ppf_unpack_subints) -- only the 8/16-bit samples cross PCIe."""
     eager_noise = True  # load_data computes noise_stds (pplib.py:2740-2748)
+    owns_reads = True   # read() returns a fresh device tensor
 
     def __init__(self, path, pscrunch=True):
         self.f = PSRFITSFile(path)
@@ -218,7 +219,8 @@ class PSRFITSSource:
         state = "Intensity" if (self.pmode or f.npol == 1) else f.text("pol_type")
         b = dict(nsub=nsub, npol=self.npo, nchan=f.nchan, nbin=f.nbin, freqs=m["freqs"],
                  weights=m["weights"], Ps=Ps, epochs=epochs, noise_stds=None,
-                 SNRs=np.ones((nsub, self.npo, f.nchan)), doppler_factors=np.ones(nsub),
+                 SNRs=np.ones((nsub, self.npo, f.nchan)), snr_deferred=True,
+                 doppler_factors=np.ones(nsub),
                  parallactic_angles=np.asarray(par, float), DM=float(DM),
                  dmc=int(I.dedispersed), baseline_removed=False, backend=f.text("backend"),
                  frontend=f.text("frontend"), backend_delay=float(I.be_delay), telescope=tel,

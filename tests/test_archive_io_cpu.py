@@ -1,0 +1,98 @@
+"""Archive I/O of the drivers on CPU: .npz metadata from the .npy header,
+range reads that touch only their rows, no file held open per archive, and
+get_TOAs reading a rank's shard in pieces of bounded size (VERDICT r03
+missing #3; pptoas.py:246,343 holds one archive at a time).
+
+The fit is replaced at the fit_portraits_batch boundary by the deterministic
+stand-in of test_dist_drivers_cpu (no device)."""
+import os
+import resource
+
+import numpy as np
+import pytest
+
+from tests.test_dist_drivers_cpu import DM0, fake_fit
+
+
+def _npz_archives(d, n, nsub=5, nchan=8, nbin=64):
+    from pulseportraiture_amd import archive, synth
+    from pulseportraiture_amd.mjd import MJD
+    paths = []
+    for i in range(n):
+        w = synth.make_workload(nsub, nchan, nbin, seed=80 + i % 3)
+        p = os.path.join(d, "a%03d.npz" % i)
+        archive.save_archive(p, dict(
+            subints=synth.workload_data_host(w)[:, None], freqs=w.freqs, Ps=np.full(nsub, w.P),
+            noise_stds=np.full((nsub, 1, nchan), 1.5),
+            epochs=[MJD(57000.0 + 0.01 * k) for k in range(nsub)], DM=DM0, backend="be",
+            frontend="fe", telescope="GBT", telescope_code="1"))
+        paths.append(p)
+    return paths
+
+
+def _get_toas(paths, monkeypatch, read_bytes_max=None):
+    from pulseportraiture_amd import pplib, pptoas, synth
+    monkeypatch.setattr(pptoas, "fit_portraits_batch", fake_fit)
+    monkeypatch.setattr(pptoas, "gen_gaussian_portraits_device",
+                        lambda code, params, alpha, nbin, freqs, nu_ref: np.array(
+                            [pplib.gen_gaussian_portrait(code, params, alpha,
+                                                         pplib.get_bin_centers(nbin), f, nu_ref)
+                             for f in np.atleast_2d(freqs)]))
+    gt = pptoas.GetTOAs(paths, synth.EXAMPLE_GMODEL, quiet=True)
+    if read_bytes_max is not None:
+        gt.read_bytes_max = read_bytes_max
+    gt.get_TOAs(quiet=True)
+    return [pplib.toa_line(t) for t in gt.TOA_list]
+
+
+def test_npz_meta_reads_header_only_and_ranges(tmp_path, monkeypatch):
+    from pulseportraiture_amd import archive
+    p = _npz_archives(str(tmp_path), 1, nsub=7)[0]
+    full = np.load(p)["subints"]
+    orig = np.lib.npyio.NpzFile.__getitem__
+
+    def guarded(self, key):
+        assert key != "subints", "metadata must not load DATA"
+        return orig(self, key)
+    monkeypatch.setattr(np.lib.npyio.NpzFile, "__getitem__", guarded)
+    a = archive.open_archive(p)
+    assert (a.meta.nsub, a.meta.npol, a.meta.nchan, a.meta.nbin) == (7, 1, 8, 64)
+    # stored (np.savez) member: rows lo:hi come from a memory map of the file
+    np.testing.assert_array_equal(a.read(2, 5), full[2:5])
+    np.testing.assert_array_equal(a.read(), full)
+
+
+def test_get_toas_more_archives_than_open_files(tmp_path, monkeypatch):
+    """One Archive per datafile is kept until the call returns; none of them
+    may hold a file open (with more archives than RLIMIT_NOFILE
+    later opens failed and archives were skipped without an error)."""
+    paths = _npz_archives(str(tmp_path), 60)
+    ref = None
+    soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
+    nfd = len(os.listdir("/proc/self/fd"))
+    try:
+        resource.setrlimit(resource.RLIMIT_NOFILE, (nfd + 24, hard))
+        lines = _get_toas(paths, monkeypatch)
+    finally:
+        resource.setrlimit(resource.RLIMIT_NOFILE, (soft, hard))
+    assert len(lines) == 60 * 5
+    ref = _get_toas(paths[:2], monkeypatch)
+    assert lines[:10] == ref
+
+
+@pytest.mark.parametrize("budget_subints", [1, 2, 3])
+def test_get_toas_bounded_shard_reads(tmp_path, monkeypatch, budget_subints):
+    from pulseportraiture_amd import archive
+    paths = _npz_archives(str(tmp_path), 2, nsub=5)
+    ref = _get_toas(paths, monkeypatch)
+    reads = []
+    orig = archive._Npz.read
+
+    def read(self, lo, hi):
+        reads.append(hi - lo)
+        return orig(self, lo, hi)
+    monkeypatch.setattr(archive._Npz, "read", read)
+    per = 8 * 8 * 64  # bytes of one subint (npol 1, nchan 8, nbin 64)
+    got = _get_toas(paths, monkeypatch, read_bytes_max=budget_subints * per)
+    assert got == ref  # the same TOAs, in the same order
+    assert max(reads) <= budget_subints and sum(reads) == 10
