@@ -296,7 +296,9 @@ def leg_ppalign(eng, narch, niter, seed):
     archive.register_archive("bench_pa_guess", dict(subints=w.model[None, None], freqs=w.freqs,
                                                     Ps=[w.P], epochs=[(57000, 0, 0.0)],
                                                     DM=w.DM0, dmc=1))
-    ppalign.align_archives(names[:min(64, narch)], "bench_pa_guess", niter=1, quiet=True)
+    # warm-up: the same call at niter 1 (device workspace and the caching
+    # allocator reach their steady-state sizes outside the timed call)
+    ppalign.align_archives(names, "bench_pa_guess", niter=1, quiet=True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     port = ppalign.align_archives(names, "bench_pa_guess", fit_dm=True, niter=niter, quiet=True)

@@ -148,8 +148,8 @@ def profile_snr(rows, duty=0.15, threshold=0.1):
     forms them (window sums bin by bin from the start; the running power in
     64 contiguous segments, then the segment totals in order), so discrete
     choices (window, edges) are the device's on the same rows."""
-    x = np.atleast_2d(np.asarray(rows, dtype=float))
     shape = np.shape(rows)[:-1]
+    x = np.asarray(rows, dtype=float).reshape(-1, np.shape(rows)[-1])
     nrow, nbin = x.shape
     width = max(1, int(duty * nbin))
     out = np.zeros(nrow)

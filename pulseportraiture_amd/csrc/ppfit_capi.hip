@@ -545,7 +545,8 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
       return r;
     if (!ctx->active_h) HIPCHK(ctx, hipHostMalloc(&ctx->active_h, sizeof(int)));
   }
-  const size_t lds_guess = (size_t)NHP * sizeof(double2);
+  const size_t lds_guess =
+      (size_t)(NHP + (d->guess ? pfa_scratch_slots(d->guess_Ns, NH) : 0)) * sizeof(double2);
   // Phase-family Taylor path, several pieces per chunk on two queues: piece
   // p's data pass starts when piece p-1's has finished, so the latency-bound
   // guess / fit / post-fit kernels of one piece run beside the HBM-bound
@@ -1070,16 +1071,23 @@ int ppf_rotate_accumulate(ppf_ctx* ctx, int32_t nsub, int32_t nchan, int32_t nbi
   const double2* tw;
   if (int r = twiddles(ctx, nbin, &tw)) return r;
   const int NH = nbin / 2 + 1;
-  int nsplit = (2048 + nchan - 1) / nchan;
+  // nbin 2048: one wave per row (register FFT), workgroups of four channels,
+  // about 8 waves per SIMD; else one workgroup per (slice, channel)
+  const bool wave = logN == 10;
+  int nsplit = wave ? (8192 + nchan - 1) / nchan : (2048 + nchan - 1) / nchan;
   if (nsplit > nsub) nsplit = nsub;
   if (nsplit < 1) nsplit = 1;
   const size_t count = (size_t)nchan * NH;
   if (int r = ensure(ctx, ctx->aux, (size_t)nsplit * count * sizeof(double2))) return r;
   double2* partial = reinterpret_cast<double2*>(ctx->aux.p);
   if (int r = timed(ctx, PPF_K_ROT_ACCUM, [&] {
-        LOGN_SWITCH(logN, hipLaunchKernelGGL(k_rot_accum<LG>, dim3(nsplit * nchan), dim3(kBlock),
-                                             0, ctx->stream, data, phase, weight, partial, nsub,
-                                             nchan, nsplit, tw));
+        if (wave)
+          hipLaunchKernelGGL(k_rot_accum_w, dim3(nsplit * ((nchan + 3) / 4)), dim3(256), 0,
+                             ctx->stream, data, phase, weight, partial, nsub, nchan, nsplit, tw);
+        else
+          LOGN_SWITCH(logN, hipLaunchKernelGGL(k_rot_accum<LG>, dim3(nsplit * nchan),
+                                               dim3(kBlock), 0, ctx->stream, data, phase, weight,
+                                               partial, nsub, nchan, nsplit, tw));
       }))
     return r;
   double2* acc = reinterpret_cast<double2*>(accum);

@@ -993,8 +993,11 @@ __device__ void guess_subint(const FitArgs& a, int c, int s, unsigned char* dyn,
   // err = get_noise(rot_prof) * sqrt(nbin/2), pplib.py:2076-2080
   const double noise = sqrt(pno / (double)a.nbin / (double)(a.NH - a.kc));
   const double err2 = noise * noise * (0.5 * (double)a.nbin);
+  // the prime-factor grid's scratch follows rm in the dynamic LDS
+  // (ppf_fit_portrait_batch sizes it with pfa_scratch_slots)
   guess_search(rm, a.NH, 1.0 / err2, a.Ns, -0.5, 0.5, gs, !(a.solver_flags & PPF_GUESS_DIRECT),
-               a.ptime ? a.ptime + 10 : nullptr);
+               a.ptime ? a.ptime + 10 : nullptr,
+               pfa_scratch_slots(a.Ns, a.NH) ? rm + a.NHP : nullptr);
   if (tid == 0) {
     double nug = a.guess_nu ? a.guess_nu[s] : NAN;
     if (isnan(nug)) nug = fmean;
@@ -1338,6 +1341,15 @@ __global__ void k_model_mean(const double2* __restrict__ M, double2* __restrict_
 __device__ __forceinline__ double dot8(double a, double b) {
   return lane0(group8_sum(a * b));
 }
+// scipy's ScalarFunction memoises the last point it evaluated
+// (_differentiable_functions.py: fun(x) re-evaluates only when x differs,
+// np.array_equal): a trust-ncg proposal bitwise equal to the last evaluated
+// point -- after a rejection the interior Steihaug step is often the same
+// step again -- reuses its f (and g, H) and does not count in nfev.  Lane
+// i < 5 holds component i of both points; wave-uniform result.
+__device__ __forceinline__ bool same_point8(int lane, double p, double e) {
+  return lane0(group8_sum((lane < 5 && !(p == e)) ? 1.0 : 0.0)) == 0.0;
+}
 __device__ __forceinline__ double hvec(const double (&Hrow)[5], double v) {
   double s = 0.0;
   s += Hrow[0] * lane_at<0>(v);
@@ -1415,6 +1427,7 @@ struct SolveShared {
   double out[48];
   double red[kWaves][48];
   int done, nok, slot;  // slot: accumulator half holding the accepted point
+  int same;             // the proposal repeats the last evaluated point
 };
 
 template <bool SCAT>
@@ -1438,6 +1451,7 @@ __global__ __launch_bounds__(kBlock) void k_solve(FitArgs a) {
   double f = 0.0, g = 0.0, xl = 0.0, Hrow[5] = {0, 0, 0, 0, 0};
   double tr = 1.0, predv = 0.0, pl = 0.0;
   int hits = 0, k = 0, status = (m.nok == 0) ? -1 : 0, nfev = 0;
+  double xe = 0.0;  // lane i < 5: the last evaluated point (same_point8)
   auto load_fgh = [&](double& ff, double& gg, double (&HH)[5]) {
     ff = sh.out[0];
     gg = lane < 5 ? sh.out[1 + lane] : 0.0;
@@ -1453,6 +1467,7 @@ __global__ __launch_bounds__(kBlock) void k_solve(FitArgs a) {
     if (tid < 64) {
       load_fgh(f, g, Hrow);
       xl = lane < 5 ? sh.x[lane] : 0.0;
+      xe = xl;
       nfev = 1;
       if (a.solver_flags & PPF_SOLVE_EVAL) {  // objective at init only
         status = 1;
@@ -1471,17 +1486,25 @@ __global__ __launch_bounds__(kBlock) void k_solve(FitArgs a) {
         pl = steihaug(f, g, Hrow, tr, hits);
         predv = model_val(f, g, Hrow, pl);
         if (lane < 5) sh.xp[lane] = xl + pl;
+        const bool same = same_point8(lane, xl + pl, xe);
+        if (lane == 0) sh.same = same;
       }
     }
     __syncthreads();
     if (sh.done) break;
     // every wave writes the proposal into the half the accepted point is not in
+    // (a repeat of the last evaluated point reuses its sweep: sh.out and the
+    // accumulators in that half are still its own)
+    const bool fresh = !sh.same;
     double* sl = acc0 + (size_t)(sh.slot ^ 1) * a.nchan * NACC;
-    sweep<0, SCAT>(a, m, c, s, sh.xp, refs, P, sl, sh.out, sh.red, TaylorSrc{});
+    if (fresh) sweep<0, SCAT>(a, m, c, s, sh.xp, refs, P, sl, sh.out, sh.red, TaylorSrc{});
     if (tid < 64) {
       double fp, gp, Hp[5] = {0, 0, 0, 0, 0};
       load_fgh(fp, gp, Hp);
-      nfev += 1;
+      if (fresh) {
+        nfev += 1;
+        xe = xl + pl;
+      }
       const double actual = f - fp;
       const double pred = f - predv;
       if (pred <= 0.0) {
@@ -1600,8 +1623,37 @@ __global__ __launch_bounds__(64) void k_scat_step(FitArgs a, const double* part,
   int hits, k, status, nfev, slot;
   bool done = false;
   // solver trace (ppf_set_trace): the point this sweep evaluated, its f, g, H
-  double xev = lane < 5 ? (init ? st.x[lane] : st.xp[lane]) : 0.0;
+  const double xev = lane < 5 ? (init ? st.x[lane] : st.xp[lane]) : 0.0;
   double rho_tr = NAN, pred_tr = NAN;
+  // k_solve's post-sweep block for the point xev (whose f, g, H are in out);
+  // counted: a fresh sweep (scipy's nfev), else a repeat of the same point
+  auto advance = [&](bool counted) {
+    double fp, gp, Hp[5] = {0, 0, 0, 0, 0};
+    load_fgh(fp, gp, Hp);
+    if (counted) nfev += 1;
+    const double actual = f - fp;
+    const double pred = f - predv;
+    pred_tr = pred;
+    if (pred <= 0.0) {
+      status = 2;
+      done = true;
+    } else {
+      const double rho = actual / pred;
+      rho_tr = rho;
+      if (rho < 0.25) tr *= 0.25;
+      else if (rho > 0.75 && hits) tr = fmin(2.0 * tr, 1000.0);
+      if (rho > 0.15) {
+        xl = xl + pl;
+        f = fp;
+        g = gp;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) Hrow[j] = Hp[j];
+        slot ^= 1;
+      }
+      k += 1;
+      if (k >= 1000) { status = 1; done = true; }
+    }
+  };
   if (init) {
     load_fgh(f, g, Hrow);
     xl = lane < 5 ? st.x[lane] : 0.0;
@@ -1626,32 +1678,7 @@ __global__ __launch_bounds__(64) void k_scat_step(FitArgs a, const double* part,
     status = st.status;
     nfev = st.nfev;
     slot = st.slot;
-    // k_solve's post-sweep block
-    double fp, gp, Hp[5] = {0, 0, 0, 0, 0};
-    load_fgh(fp, gp, Hp);
-    nfev += 1;
-    const double actual = f - fp;
-    const double pred = f - predv;
-    pred_tr = pred;
-    if (pred <= 0.0) {
-      status = 2;
-      done = true;
-    } else {
-      const double rho = actual / pred;
-      rho_tr = rho;
-      if (rho < 0.25) tr *= 0.25;
-      else if (rho > 0.75 && hits) tr = fmin(2.0 * tr, 1000.0);
-      if (rho > 0.15) {
-        xl = xl + pl;
-        f = fp;
-        g = gp;
-#pragma unroll
-        for (int j = 0; j < 5; ++j) Hrow[j] = Hp[j];
-        slot ^= 1;
-      }
-      k += 1;
-      if (k >= 1000) { status = 1; done = true; }
-    }
+    advance(true);
   }
   if (a.trace && nok) {
     double xv[5];
@@ -1667,15 +1694,21 @@ __global__ __launch_bounds__(64) void k_scat_step(FitArgs a, const double* part,
       r[31] = (double)hits;  // the Steihaug boundary flag of the step that led here
     }
   }
-  if (!done) {  // k_solve's loop head: NaN gradient, else the next proposal
+  // k_solve's loop head: NaN gradient, else the next proposal; a proposal
+  // that repeats xev (the point just evaluated) is decided on its memoised
+  // f, g, H without a sweep and without counting, as scipy's ScalarFunction
+  // does, until a new point (for the next sweep) or the end
+  while (!done) {
     const double jm = sqrt(dot8(g, g));
     if (!(jm >= -1.0)) {
       status = 0;
       done = true;
-    } else {
-      pl = steihaug(f, g, Hrow, tr, hits);
-      predv = model_val(f, g, Hrow, pl);
+      break;
     }
+    pl = steihaug(f, g, Hrow, tr, hits);
+    predv = model_val(f, g, Hrow, pl);
+    if (!same_point8(lane, xl + pl, xev)) break;
+    advance(false);
   }
   // state back (lanes < 5 own the vectors; lane 0 the scalars)
   if (lane < 5) {

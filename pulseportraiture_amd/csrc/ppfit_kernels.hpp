@@ -285,9 +285,144 @@ __device__ __forceinline__ double brute_pass(const double2* rm, int NH, double i
   return myf;
 }
 
+// Prime-factor split of the grid DFT length L = A B (A, B coprime, B <=
+// kPfaMax, the most balanced such pair): the get_TOAs / ppalign grids with
+// Ns = nbin (L = nbin - 1: 2047 = 23 x 89, 1023 = 31 x 33, 4095 = 63 x 65,
+// 511 = 7 x 73, 255 = 15 x 17) take two passes of short DFTs instead of
+// Ns x NH phasor terms.  false: no such split (L prime, or too long).
+constexpr int kPfaMax = 256, kPfaPer = 16;  // <= kPfaPer grid values per thread
+__host__ __device__ inline bool pfa_split(int L, int& A, int& B) {
+  A = B = 0;
+  if (L < 6 || L > kBlock * kPfaPer) return false;
+  int best = 1 << 30;
+  for (int a = 2; a * a <= L; ++a) {
+    if (L % a) continue;
+    const int b = L / a;
+    int x = a, y = b;
+    while (y) { const int t = x % y; x = y; y = t; }
+    if (x != 1 || b > kPfaMax) continue;
+    if (a + b < best) { best = a + b; A = a; B = b; }
+  }
+  return A > 0;
+}
+// LDS scratch (double2 slots) guess_search needs for the PFA grid of Ns
+// points on (-1/2, 1/2): Y [L] plus the A- and B-point roots of unity; 0 when
+// the grid is not taken that way
+__host__ __device__ inline int pfa_scratch_slots(int Ns, int NH) {
+  const int L = Ns - 1;
+  int A, B;
+  if (L <= kBlock / 2 && NH > 2 * L) return 0;  // the folded direct grid
+  return pfa_split(L, A, B) ? L + A + B : 0;
+}
+
+// Brute-force grid on (-1/2, 1/2) by the prime-factor DFT: with phi_g =
+// -1/2 + g / L, f(phi_g) = -Re sum_{j < L} b_j w^{j g} / err^2, b_j =
+// sum_{k = j mod L} (-1)^k rm_k, w = e^{2 pi i / L}.  Good-Thomas: j = (B n1
+// + A n2) mod L, g = (B (B^-1 mod A) k1 + A (A^-1 mod B) k2) mod L, so
+// w^{j g} = W_A^{n1 k1} W_B^{n2 k2}: Y[n1][k2] = sum_n2 b_j W_B^{n2 k2}, then
+// sum_n1 Y[n1][k2] W_A^{n1 k1}.  Each thread keeps its grid values; returns
+// (via gs) the argmin as brute_pass does, and whether another grid point is
+// within rounding (1e-12 relative) of it -- then the caller re-takes the grid
+// by direct sums, as for the folded grid.
+__device__ inline bool pfa_pass(const double2* rm, int NH, double ie2, int Ns, double lo,
+                                double hi, GuessShared& gs, double2* scr, int A, int B) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int L = Ns - 1;
+  double2* Y = scr;
+  double2* wB = scr + L;
+  double2* wA = wB + B;
+  for (int m = tid; m < B; m += kBlock) {
+    double sn, cs;
+    sincospi(2.0 * (double)m / (double)B, &sn, &cs);
+    wB[m] = cmk(cs, sn);
+  }
+  for (int m = tid; m < A; m += kBlock) {
+    double sn, cs;
+    sincospi(2.0 * (double)m / (double)A, &sn, &cs);
+    wA[m] = cmk(cs, sn);
+  }
+  __syncthreads();
+  // stage 1: Y[n1][k2] = sum_{n2 < B} b_{(B n1 + A n2) mod L} W_B^{n2 k2}
+  for (int q = tid; q < L; q += kBlock) {
+    const int n1 = q / B, k2 = q - n1 * B;
+    int j = (B * n1) % L, m = 0;
+    double2 acc = cmk(0.0, 0.0);
+    for (int n2 = 0; n2 < B; ++n2) {
+      double2 b = cmk(0.0, 0.0);
+      for (int k = j; k < NH; k += L) b = (k & 1) ? csub(b, rm[k]) : cadd(b, rm[k]);
+      acc = cadd(acc, cmul(b, wB[m]));
+      j += A;
+      if (j >= L) j -= L;
+      m += k2;
+      if (m >= B) m -= B;
+    }
+    Y[q] = acc;
+  }
+  __syncthreads();
+  // stage 2 and the per-thread grid values
+  int Ai = 1, Bi = 1;  // B^-1 mod A, A^-1 mod B
+  while ((long long)B * Ai % A != 1) ++Ai;
+  while ((long long)A * Bi % B != 1) ++Bi;
+  const long long cB = (long long)B * Ai, cA = (long long)A * Bi;
+  double vals[kPfaPer];
+  int gi[kPfaPer];
+  double bv = NAN;
+  int bi = 0x7fffffff;
+#pragma unroll
+  for (int r = 0; r < kPfaPer; ++r) {
+    const int q = tid + r * kBlock;
+    vals[r] = NAN;
+    gi[r] = 0x7fffffff;
+    if (q < L) {
+      const int k1 = q / B, k2 = q - k1 * B;
+      double re = 0.0;
+      int m = 0;
+      for (int n1 = 0; n1 < A; ++n1) {
+        const double2 y = Y[n1 * B + k2], t = wA[m];
+        re = fma(y.x, t.x, re);
+        re = fma(-y.y, t.y, re);
+        m += k1;
+        if (m >= A) m -= A;
+      }
+      const int g = (int)((cB * k1 + cA * k2) % L);
+      const double f = -re * ie2;
+      vals[r] = f;
+      gi[r] = g;
+      if (argmin_better(f, g, bv, bi)) { bv = f; bi = g; }
+    }
+  }
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double ov = __shfl_xor(bv, o);
+    const int oi = __shfl_xor(bi, o);
+    if (argmin_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+  }
+  if (lane == 0) { gs.bestv[w] = bv; gs.besti[w] = bi; }
+  __syncthreads();
+  if (tid == 0) {
+    double v = gs.bestv[0];
+    int i = gs.besti[0];
+    for (int q = 1; q < kWaves; ++q)
+      if (argmin_better(gs.bestv[q], gs.besti[q], v, i)) { v = gs.bestv[q]; i = gs.besti[q]; }
+    const double step = (hi - lo) / (double)(Ns - 1);
+    gs.x0 = (i == Ns - 1) ? hi : __dadd_rn(__dmul_rn((double)i, step), lo);
+    gs.bestv[0] = v;
+    gs.besti[0] = i;
+  }
+  __syncthreads();
+  const double v = gs.bestv[0];
+  const int i = gs.besti[0];
+  bool near = false;
+#pragma unroll
+  for (int r = 0; r < kPfaPer; ++r)
+    if (gi[r] != 0x7fffffff && gi[r] != i && !(fabs(vals[r] - v) > 1e-12 * fabs(v))) near = true;
+  return __syncthreads_or(near);
+}
+
 __device__ inline void guess_search(const double2* rm, int NH, double ie2, int Ns, double lo,
                                     double hi, GuessShared& gs, bool allow_fold = true,
-                                    unsigned long long* clk = nullptr) {
+                                    unsigned long long* clk = nullptr,
+                                    double2* pfa_scr = nullptr) {
   const int tid = threadIdx.x;
   // diagnostic clocks (ppf_phase_profile): [0] brute force, [1] Nelder-Mead, [2] NM calls
   const unsigned long long c0 = clk ? wall_clock64() : 0ull;
@@ -330,7 +465,11 @@ __device__ inline void guess_search(const double2* rm, int NH, double ie2, int N
     const bool near = tid < Ns && tid != i && !endpair && !(fabs(myf - v) > 1e-12 * fabs(v));
     if (__syncthreads_or(near)) brute_pass<false>(rm, NH, ie2, Ns, lo, hi, gs);
   } else {
-    brute_pass<false>(rm, NH, ie2, Ns, lo, hi, gs);
+    int A = 0, B = 0;
+    const bool pfa = pfa_scr && allow_fold && lo == -0.5 && hi == 0.5 &&
+                     pfa_scratch_slots(Ns, NH) > 0 && pfa_split(L, A, B);
+    if (!pfa || pfa_pass(rm, NH, ie2, Ns, lo, hi, gs, pfa_scr, A, B))
+      brute_pass<false>(rm, NH, ie2, Ns, lo, hi, gs);
   }
   const unsigned long long c1 = clk ? wall_clock64() : 0ull;
   // ---- Nelder-Mead polish: every thread runs the (uniform, scalar) simplex
@@ -459,6 +598,8 @@ template <int LOGN>
 __global__ void k_rot_accum(const double* data, const double* phase, const double* weight,
                             double2* partial, int nsub, int nchan, int nsplit,
                             const double2* tw);
+__global__ void k_rot_accum_w(const double* data, const double* phase, const double* weight,
+                              double2* partial, int nsub, int nchan, int nsplit, const double2* tw);
 __global__ void k_accum_reduce(const double2* partial, double2* accum, int nsplit, size_t count);
 template <int LOGN> __global__ void k_resid_chi2(ResidArgs a, const double2* tw);
 __global__ void k_vpow(double2* vp, int N, int rows);

@@ -640,6 +640,84 @@ __global__ __launch_bounds__(kBlock) void k_rot_accum(const double* __restrict__
   }
 }
 
+// The same sum for nbin = 2048 (ppalign at config 5): one wave per channel
+// row, as the data pass streams them (fft1024_wave, next row in flight in
+// registers).  Workgroup (g, p) takes channels 4 g .. 4 g + 3 of subint slice
+// p, so its four waves read adjacent rows; each lane keeps the harmonics
+// k = lane + 64 i and N - k (i <= 8) of its channel's sum in registers.  The
+// rotation e^{2 pi i k ph} w follows the data pass's guess phasor chain
+// (turn_phasor at lane, 64 and N, stepped per pair iteration).
+__global__ __launch_bounds__(256, 2) void k_rot_accum_w(const double* __restrict__ data,
+                                                       const double* __restrict__ phase,
+                                                       const double* __restrict__ weight,
+                                                       double2* __restrict__ partial, int nsub,
+                                                       int nchan, int nsplit,
+                                                       const double2* __restrict__ tw) {
+  constexpr int LOGN = 10, N = 1 << LOGN, NPI = (N / 2 + 1 + 63) / 64;
+  __shared__ double2 bufs[4][kFft1024Slots];
+  __shared__ Fft1024Tw ftw;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ngrp = (nchan + 3) / 4;
+  const int g = blockIdx.x % ngrp, p = blockIdx.x / ngrp;
+  const int n = 4 * g + w;
+  const int per = (nsub + nsplit - 1) / nsplit;
+  const int s0 = p * per, s1 = min(nsub, s0 + per);
+  ftw.fill(tw, tid, 256);
+  __syncthreads();
+  if (n >= nchan) return;  // no barriers below
+  double2* buf = bufs[w];
+  double2 ak[NPI], an[NPI];
+#pragma unroll
+  for (int i = 0; i < NPI; ++i) ak[i] = an[i] = cmk(0.0, 0.0);
+  double sw, cw;
+  sincospi(-(double)lane / (double)N, &sw, &cw);
+  const double2 w0 = cmk(cw, sw);  // e^{-i pi lane / N}
+  double ss, cs;
+  sincospi(-64.0 / (double)N, &ss, &cs);
+  const double2 wstep = cmk(cs, ss);
+  // next row with a non-zero weight in this slice
+  auto next = [&](int s) {
+    while (s < s1 && weight[(size_t)s * nchan + n] == 0.0) ++s;
+    return s;
+  };
+  WaveRow<LOGN> row;
+  int s = next(s0);
+  if (s < s1) row.load(data + ((size_t)s * nchan + n) * 2 * N, lane);
+  while (s < s1) {
+    const size_t r = (size_t)s * nchan + n;
+    const double wt = weight[r], ph = phase[r];
+    fft1024_wave(row.x, row.y, buf, ftw, lane);
+    const int sn = next(s + 1);
+    if (sn < s1) row.load(data + ((size_t)sn * nchan + n) * 2 * N, lane);
+    double2 e = cscale(turn_phasor((double)lane, ph), wt);
+    const double2 estep = turn_phasor(64.0, ph), EN = turn_phasor((double)N, ph);
+    double2 t = w0;
+#pragma unroll
+    for (int i = 0; i < NPI; ++i) {
+      const int k = lane + 64 * i;
+      if (i > 0) { t = cmul(t, wstep); e = cmul(e, estep); }
+      if (k <= N / 2) {
+        double2 xk, xn;
+        rfft_pair_v(buf[fft1024_slot(k)], buf[fft1024_slot((N - k) & (N - 1))], t, xk, xn);
+        ak[i] = cadd(ak[i], cmul(xk, e));
+        if (k < N / 2) an[i] = cadd(an[i], cmul(xn, cmul(EN, cconj(e))));
+      }
+    }
+    fft_sync<true>();  // every lane's reads of buf done before the next FFT
+    s = sn;
+  }
+  double2* out = partial + ((size_t)p * nchan + n) * (N + 1);
+#pragma unroll
+  for (int i = 0; i < NPI; ++i) {
+    const int k = lane + 64 * i;
+    if (k <= N / 2) {
+      out[k] = ak[i];
+      if (k < N / 2) out[N - k] = an[i];  // k = 0: the Nyquist harmonic
+    }
+  }
+}
+
 __global__ void k_accum_reduce(const double2* __restrict__ partial, double2* __restrict__ accum,
                                int nsplit, size_t count) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -308,6 +308,7 @@ struct TaylorShared {
   double red[kWaves][48];
   double ifact[kMT];  // c_inv_fact for taylor_cells
   int done, nok, slot, tslot, q, mvalid;
+  int same;  // the proposal repeats the last evaluated point (same_point8)
 };
 
 // T slot 0 of subint c into the kernel's LDS copy (all threads; the caller
@@ -411,6 +412,7 @@ __global__ __launch_bounds__(kBlock, 3) void k_fit_taylor(FitArgs a) {
   double f = 0.0, g = 0.0, xl = 0.0, Hrow[5] = {0, 0, 0, 0, 0};
   double tr = 1.0, predv = 0.0, pl = 0.0;
   int hits = 0, k = 0, status = (m.nok == 0) ? -1 : 0, nfev = 0;
+  double xe = 0.0;  // lane i < 5: the last evaluated point
   auto load_fgh = [&](double& ff, double& gg, double (&HH)[5]) {
     ff = sh.out[0];
     gg = lane < 5 ? sh.out[1 + lane] : 0.0;
@@ -477,7 +479,9 @@ __global__ __launch_bounds__(kBlock, 3) void k_fit_taylor(FitArgs a) {
     if (tid < 64) {
       load_fgh(f, g, Hrow);
       xl = lane < 5 ? sh.x[lane] : 0.0;
+      xe = xl;
       nfev = 1;
+      trace_sweep(a, s, 0, sh.x, sh.out, 21, true);
       if (a.solver_flags & PPF_SOLVE_EVAL) {  // objective at init only
         status = 1;
         if (lane == 0) sh.done = 1;
@@ -497,23 +501,34 @@ __global__ __launch_bounds__(kBlock, 3) void k_fit_taylor(FitArgs a) {
         predv = model_val(f, g, Hrow, pl);
         const double pv = xl + pl;  // lane i < 5: component i of the proposal
         if (lane < 5) sh.xp[lane] = pv;
-        const int qp = pick(__shfl(pv, 0), __shfl(pv, 1), __shfl(pv, 2));
-        if (lane == 0) sh.q = qp;
+        const bool same = same_point8(lane, pv, xe);
+        const int qp = same ? sh.q : pick(__shfl(pv, 0), __shfl(pv, 1), __shfl(pv, 2));
+        if (lane == 0) {
+          sh.q = qp;
+          sh.same = same;
+        }
       }
     }
     __syncthreads();
     mark(4);
     if (sh.done) break;
+    // a repeat of the last evaluated point reuses its sweep (sh.out, the
+    // accumulator half and the centre are still its own)
+    const bool fresh = !sh.same;
     int q = sh.q;
-    if (q < 0) q = recentre(sh.xp);
+    if (fresh && q < 0) q = recentre(sh.xp);
     mark(2);
     double* sl = acc0 + (size_t)(sh.slot ^ 1) * a.nchan * NACC;
-    sweep<0, false>(a, m, c, s, sh.xp, refs, P, sl, sh.out, sh.red, source(q));
+    if (fresh) sweep<0, false>(a, m, c, s, sh.xp, refs, P, sl, sh.out, sh.red, source(q));
     mark(3);
     if (tid < 64) {
       double fp, gp, Hp[5] = {0, 0, 0, 0, 0};
       load_fgh(fp, gp, Hp);
-      nfev += 1;
+      if (fresh) {
+        nfev += 1;
+        xe = xl + pl;
+        trace_sweep(a, s, nfev - 1, sh.xp, sh.out, 21, true);
+      }
       const double actual = f - fp;
       const double pred = f - predv;
       if (pred <= 0.0) {

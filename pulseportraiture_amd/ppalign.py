@@ -76,10 +76,22 @@ def _open_all(datafiles, model_data, SNR_cutoff, quiet, skip_these, tscrunch, ps
     return out
 
 
+class _All(np.ndarray):
+    """Marker type of the shared every-channel index array (_units)."""
+
+
+ALL = None  # set per call: np.arange(nchan) viewed as _All
+
+
 def _units(opened, model_data):
-    """(name, subint, ichans, model_ichans) per ok subint (ppalign.py:153-177)."""
+    """(name, subint, ichans, model_ichans) per ok subint (ppalign.py:153-177).
+    A unit whose channels are all the template's (every channel on in both)
+    carries the one shared index array ALL (its intersect1d)."""
     units = []
     mf = model_data.freqs[0]
+    nch = len(mf)
+    mok = model_data.ok_ichans[0]
+    model_full = len(mok) == nch
     for name, a in opened:
         m = a.meta
         try:
@@ -89,8 +101,12 @@ def _units(opened, model_data):
             same = False
         for isub in m.ok_isubs:
             if same:
-                ichans = np.intersect1d(m.ok_ichans[isub], model_data.ok_ichans[0])
-                mich = ichans
+                oi = m.ok_ichans[isub]
+                if model_full and len(oi) == nch:  # ok_ichans are sorted, unique
+                    ichans = mich = ALL
+                else:
+                    ichans = np.intersect1d(oi, mok)
+                    mich = ichans
             else:
                 ichans = np.asarray(m.ok_ichans[isub])
                 mich = np.array([np.argmin(abs(mf - m.freqs[isub, c])) for c in ichans])
@@ -98,18 +114,69 @@ def _units(opened, model_data):
     return units
 
 
+def _guess_fit_freq_rows(freqs, snrs):
+    """guess_fit_freq per row (pplib.py:2618-2632) for rows of equal length:
+    numpy's row sums of a C-order 2-D array are its 1-D sums, so each value
+    is the one guess_fit_freq(freqs[i], snrs[i]) returns."""
+    f = np.ascontiguousarray(freqs, dtype=np.float64)
+    w = np.ascontiguousarray(snrs, dtype=np.float64)
+    if len(f) > 1 and (f == f[0]).all() and (w == w[0]).all():  # one distinct row
+        return np.full(len(f), guess_fit_freq(f[0], w[0]))
+    nu0 = (f.min(axis=1) + f.max(axis=1)) * 0.5
+    f2 = f ** -2
+    return nu0 + np.sum((f - nu0[:, None]) * w * f2, axis=1) / np.sum(w * f2, axis=1)
+
+
+def _is_full(ichans, mich, full_rows):
+    """A unit with every channel of the template, in template order."""
+    if isinstance(ichans, _All):
+        return True
+    return len(ichans) == len(full_rows) and np.array_equal(mich, full_rows) and \
+        np.array_equal(ichans, mich)
+
+
+def _elem_stride(rows):
+    return (rows[1].data_ptr() - rows[0].data_ptr()) // rows[0].element_size() \
+        if len(rows) > 1 else rows[0][0].numel()
+
+
+def _uniform_rows(rows):
+    """rows [npol=1, nchan, nbin] tensors that are equally spaced views of one
+    storage (each contiguous, same device/dtype, positive stride)."""
+    r0 = rows[0]
+    if r0.dim() != 3 or r0.shape[0] != 1 or not r0.is_contiguous() or \
+            r0.dtype != torch.float64:
+        return False
+    if len(rows) == 1:
+        return True
+    st = rows[1].data_ptr() - r0.data_ptr()
+    if st < r0.numel() * r0.element_size() or st % r0.element_size():
+        return False
+    base = r0.untyped_storage().data_ptr()
+    p0 = r0.data_ptr()
+    for j, r in enumerate(rows):
+        if r.data_ptr() != p0 + j * st or not r.is_contiguous() or r.shape != r0.shape or \
+                r.device != r0.device or r.untyped_storage().data_ptr() != base:
+            return False
+    return True
+
+
 class _UnitStack:
     """Device-resident inputs of this rank's units, built once and reused by
     every iteration (the reference re-reads every archive per iteration,
     ppalign.py:121-127; the data do not change): unit channel c sits in
-    template slot mich[c], other slots are masked."""
+    template slot mich[c], other slots are masked.  Units whose channels are
+    the template's own (every channel, same order) are gathered with one
+    device copy for all of them -- none when they already are equally spaced
+    rows of one tensor -- and their host arrays stacked row-wise; the others
+    take the per-channel path."""
 
     def __init__(self, eng, units, opened, model_freqs, npol, nchan, nbin):
         dev = eng.device
         n = len(units)
         f64 = dict(dtype=torch.float64, device=dev)
         self.n = n
-        self.pols = [torch.zeros((n, nchan, nbin), **f64) for _ in range(npol)]
+        self.pols = [None] * npol
         freqs = np.tile(np.asarray(model_freqs, dtype=np.float64), (n, 1))
         errs = np.ones((n, nchan))
         mask = np.zeros((n, nchan), dtype=np.uint8)
@@ -120,11 +187,19 @@ class _UnitStack:
         by_arch = {}
         for i, u in enumerate(units):
             by_arch.setdefault(u[0], []).append(i)
+        full_rows = np.arange(nchan)
+        frow, fsrc = [], []  # full units: stack row i <- (tensor, subint row)
+        # the stack is allocated unless every unit is a full row of one
+        # strided tensor (decided once all units are seen)
+        partial_units = [i for i, u in enumerate(units) if not _is_full(u[2], u[3], full_rows)]
+        if partial_units or npol != 1:
+            self.pols = [torch.empty((n, nchan, nbin), **f64) for _ in range(npol)]
+        full_i, full_f, full_w, full_s, full_e = [], [], [], [], []
         for name, idx in by_arch.items():
             a = arch[name]
             m = a.meta
-            isubs = [units[i][1] for i in idx]
-            lo, hi = min(isubs), max(isubs) + 1
+            isubs = np.array([units[i][1] for i in idx])
+            lo, hi = int(isubs.min()), int(isubs.max()) + 1
             sub = a.read(lo, hi)  # this rank's subint range only
             if not isinstance(sub, torch.Tensor):
                 sub = torch.as_tensor(np.ascontiguousarray(sub), device=dev)
@@ -133,29 +208,61 @@ class _UnitStack:
                 snrs = np.array(m.SNRs, dtype=np.float64)
                 snrs[lo:hi] = a.snrs(sub)
             ns = m.get("noise_stds")
+            ns = None if ns is None else np.asarray(ns)
+            # device rows, and the host arrays of this archive's units (full
+            # units as row views, stacked once for all archives below)
             for i in idx:
                 _, isub, ichans, mich = units[i]
-                full = len(ichans) == nchan and np.array_equal(mich, np.arange(nchan)) and \
-                    np.array_equal(ichans, mich)
-                if full:
-                    for ipol in range(npol):
-                        self.pols[ipol][i].copy_(sub[isub - lo, ipol])
-                else:
-                    ic = torch.as_tensor(ichans, device=dev, dtype=torch.long)
-                    mc = torch.as_tensor(mich, device=dev, dtype=torch.long)
-                    for ipol in range(npol):
-                        self.pols[ipol][i].index_copy_(0, mc,
-                                                       sub[isub - lo, ipol].index_select(0, ic))
+                P[i] = m.Ps[isub]
+                DMg[i] = m.DM
+                if _is_full(ichans, mich, full_rows):
+                    frow.append(i)
+                    fsrc.append(sub[isub - lo])
+                    full_i.append(i)
+                    full_f.append(m.freqs[isub])
+                    full_w.append(m.weights[isub])
+                    full_s.append(snrs[isub, 0])
+                    if ns is not None:
+                        full_e.append(ns[isub, 0])
+                    else:
+                        full_e.append(None)
+                    continue
+                ic = torch.as_tensor(ichans, device=dev, dtype=torch.long)
+                mc = torch.as_tensor(mich, device=dev, dtype=torch.long)
+                for ipol in range(npol):
+                    self.pols[ipol][i].zero_()
+                    self.pols[ipol][i].index_copy_(0, mc, sub[isub - lo, ipol].index_select(0, ic))
                 freqs[i, mich] = m.freqs[isub, ichans]
                 if ns is not None:
-                    errs[i, mich] = np.asarray(ns)[isub, 0, ichans]
+                    errs[i, mich] = ns[isub, 0, ichans]
                 else:
                     need_noise[i] = True
                 mask[i, mich] = 1
                 wts[i, mich] = m.weights[isub, ichans]
-                P[i] = m.Ps[isub]
-                DMg[i] = m.DM
                 nu_fit[i] = guess_fit_freq(m.freqs[isub, ichans], snrs[isub, 0, ichans])
+        if full_i:
+            rows = np.array(full_i)
+            fr = np.stack(full_f)
+            freqs[rows] = fr
+            wts[rows] = np.stack(full_w)
+            mask[rows] = 1
+            have = np.array([e is not None for e in full_e])
+            if have.any():
+                errs[rows[have]] = np.stack([e for e in full_e if e is not None])
+            need_noise[rows[~have]] = True
+            nu_fit[rows] = _guess_fit_freq_rows(fr, np.stack(full_s))
+        if frow and npol == 1 and frow == list(range(n)) and _uniform_rows(fsrc):
+            # every unit a full row of one strided tensor (rows of the caller's
+            # own stack): use it in place, no copy
+            self.pols = [fsrc[0].as_strided((n, nchan, nbin), (_elem_stride(fsrc), nbin, 1))]
+        elif frow:  # one gather per polarisation for every full unit
+            if self.pols[0] is None:
+                self.pols = [torch.empty((n, nchan, nbin), **f64) for _ in range(npol)]
+            dst = torch.as_tensor(np.array(frow), device=dev, dtype=torch.long)
+            src = torch.stack(fsrc)  # [nfull, npol, nchan, nbin]
+            for ipol in range(npol):
+                self.pols[ipol].index_copy_(0, dst, src[:, ipol])
+            del src
         if need_noise.any():  # load_data's noise_stds (pplib.py:2744-2748), on the device
             noise = eng.noise_rows(self.pols[0].reshape(-1, nbin)).reshape(n, nchan).cpu().numpy()
             errs = np.where(need_noise[:, None] & (mask > 0), noise, errs)
@@ -232,6 +339,8 @@ def align_archives(metafile, initial_guess, fit_dm=True, tscrunch=False, pscrunc
     rank, world = dist_info()
     skip_these = []
     opened = _open_all(datafiles, model_data, SNR_cutoff, quiet, skip_these, tscrunch, pscrunch)
+    global ALL
+    ALL = np.arange(nchan).view(_All)
     units = _units(opened, model_data)
     t0 = mark("open", t0)
     lo, hi = shard_range(len(units), rank, world)

@@ -1,8 +1,8 @@
 """The sharded drivers with the real device path: two ranks on the one GPU of
 the box (gloo process group -- RCCL refuses two ranks on one device), each
-fitting its own shard through libppfit.  GetTOAs.get_TOAs must give every
-rank the single-process TOAs (pptoas.py:246,343 sharded, all_gather_object
-of the result rows), and ppalign.align_archives the single-process template
+fitting its own shard through libppfit.  GetTOAs.get_TOAs must give rank 0
+the single-process TOAs (pptoas.py:246,343 sharded, the result arrays
+gathered to rank 0; the other rank holds none), and ppalign.align_archives the single-process template
 (sharded fits and rotate-accumulate, one fused all_reduce of the Fourier-
 domain sum, ppalign.py:113-213).  tests/test_dist_drivers_cpu.py covers the
 same bookkeeping on CPU with the fit replaced; here nothing is replaced.
@@ -81,10 +81,12 @@ def test_drivers_two_ranks_on_device_equal_single_process():
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_worker, args=(2, _free_port(), d), nprocs=2, join=True)
         got = [np.load(os.path.join(d, "r%d.npz" % k)) for k in range(2)]
+    # the same batched device fits on a subset of subints: identical lines on
+    # rank 0, which assembles every TOA (GetTOAs.gather_to = "root")
+    assert list(got[0]["lines"]) == ref_lines
+    np.testing.assert_array_equal(got[0]["ddm"], ref_ddm)
+    assert len(got[1]["lines"]) == 0
     for g in got:
-        # the same batched device fits on a subset of subints: identical lines
-        assert list(g["lines"]) == ref_lines
-        np.testing.assert_array_equal(g["ddm"], ref_ddm)
         # the template is a sum over ranks (different fp64 addition order)
         np.testing.assert_allclose(g["tmpl"], ref_tmpl, rtol=0,
                                    atol=1e-12 * np.abs(ref_tmpl).max())

@@ -145,10 +145,13 @@ def test_synth_matches_numpy(eng):
     np.testing.assert_allclose(got, ref, atol=1e-11)
 
 
-def test_rotate_accumulate(eng):
+@pytest.mark.parametrize("nsub,nchan,nbin", [(5, 6, 128), (37, 10, 2048), (3, 3, 2048)])
+def test_rotate_accumulate(eng, nsub, nchan, nbin):
+    """Fourier-domain rotate-and-sum of ppalign (ppalign.py:202-208); nbin 2048
+    takes the one-wave-per-row register-FFT kernel (k_rot_accum_w), including
+    a channel count that leaves a workgroup's last waves without a row."""
     import torch
     rng = np.random.default_rng(9)
-    nsub, nchan, nbin = 5, 6, 128
     data = rng.normal(0, 1, (nsub, nchan, nbin))
     ph = rng.uniform(-1, 1, (nsub, nchan))
     w = rng.uniform(0, 2, (nsub, nchan))

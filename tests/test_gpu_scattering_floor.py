@@ -1,21 +1,35 @@
 """Config 3 at its own shape against the reference: 200 of bench.py's
 scattering subints (512 x 1024, phi + DM + log10 tau + alpha, get_TOAs' guess
-and trust-ncg), fitted on the device and by the reference
-(tests/golden/scattering_200.npz, make_golden_cfg3.py: the reference's
-get_TOAs per-subint flow, pptoas.py:383-488, plus four restarts one ulp
-away in phase and log10 tau).
+and trust-ncg), fitted on the device and by the reference.
 
-What holds, and is asserted:
-* the guess (init phase) and every status are the reference's;
-* every device end point is as good a minimum as the reference's:
-  |chi^2_device - chi^2_reference| <= 1e-3 (one sigma in one parameter
-  moves chi^2 by 1);
-* at least 85 % of the end points are within 1e-3 sigma of the reference's.
-The rest are subints on which trust-ncg's stopping test (predicted
-reduction <= 0, status 2) or the basin it settles in is decided by rounding:
-the reference itself moves by > 1e-3 sigma under one-ulp restarts on 23 of
-these 200 subints (up to 24 sigma), and the device ends within 2.2e-4 of the
-reference's chi^2 wherever its parameters differ.  Every comparison prints.
+Fixtures (the reference's own get_TOAs per-subint flow, pptoas.py:383-488,
+through the SURVEY §8(c) shim):
+* scattering_200.npz (make_golden_cfg3.py): the reference's init, end point,
+  errors, status, nfev, red chi2, and four restarts one ulp away in phase
+  and log10 tau;
+* scattering_200_perm.npz (make_golden_cfg3_perm.py): the same fits with the
+  channels in 8 seeded random orders -- every per-channel term the same
+  number, only the order of the reference's own channel sums changed.
+
+trust-ncg with gtol = -1 (pptoaslib.py:1002) stops at the first predicted
+reduction <= 0, i.e. when its trust radius has collapsed onto rounding; on
+42 of these 200 subints the reference itself ends more than 1e-3 sigma away
+from its own answer under a reordering of its sums (up to 46 sigma in phi: the
+end points differ by ~1e-2 sigma in DM, tau, alpha, and the zero-covariance
+frequency nu_DM the phase is reported at moves with them).  Those end points
+are discrete: the device lands on them.
+
+Asserted, per subint:
+* the guess (init phase) and the status are the reference's;
+* nfev (scipy's count: a proposal equal to the last evaluated point is not
+  re-evaluated) is within 2 of the reference's;
+* |chi^2_device - chi^2_reference| <= 1e-3;
+* the end point is within 1e-3 sigma of the reference's, or of one of the
+  reference's own end points under a one-ulp restart or a channel
+  reordering, or -- where the device stops between them -- no farther from
+  the reference than the reference's own spread;
+* where the reference's own spread is below 1e-3 sigma, within 1e-3 sigma of
+  the reference.
 """
 import os
 
@@ -26,6 +40,8 @@ from tests.conftest import GOLDEN
 from tests.golden_consts import DM0
 
 pytestmark = pytest.mark.gpu
+
+PARAMS = ["phi", "DM", "tau", "alpha"]
 
 
 @pytest.fixture(scope="module")
@@ -40,6 +56,7 @@ def gpu():
 def test_scattering_200_subints_vs_reference(gpu):
     from pulseportraiture_amd import synth
     z = np.load(os.path.join(GOLDEN, "scattering_200.npz"))
+    zp = np.load(os.path.join(GOLDEN, "scattering_200_perm.npz"))
     nsub, seed = int(z["nsub"]), int(z["seed"])
     nchan, nbin, tau = 512, 1024, 2e-3
     data = synth.workload_data_host_parallel(nsub, nchan, nbin, seed=seed,
@@ -56,22 +73,35 @@ def test_scattering_200_subints_vs_reference(gpu):
     np.testing.assert_allclose(r["init_used"][:, 0], z["init_phi"], rtol=0, atol=1e-6)
     assert np.array_equal(r["status"], z["status"].astype(int)), np.where(
         r["status"] != z["status"])
-    sig = np.stack([z["phi_err"], z["DM_err"], z["tau_err"], z["alpha_err"]], 1)
-    ref = np.stack([z["phi"], z["DM"], z["tau"], z["alpha"]], 1)
+    sig = np.stack([z[c + "_err"] for c in PARAMS], 1)
+    ref = np.stack([z[c] for c in PARAMS], 1)
     dev = r["params"][:, [0, 1, 3, 4]]
     dx = (np.abs(dev - ref) / sig).max(axis=1)
-    floor = np.max([(np.abs(np.stack([z["r%d_%s" % (k, c)] for c in
-                                      ["phi", "DM", "tau", "alpha"]], 1) - ref) / sig).max(axis=1)
-                    for k in range(4)], axis=0)
+    # the reference's own end points: one-ulp restarts and channel reorderings
+    alts = [np.stack([z["r%d_%s" % (k, c)] for c in PARAMS], 1) for k in range(4)]
+    alts += [np.stack([zp["perm_" + c][:, k] for c in PARAMS], 1)
+             for k in range(int(zp["nperm"]))]
+    alts = np.stack(alts, 1)  # [nsub, nalt, 4]
+    spread = (np.abs(alts - ref[:, None]) / sig[:, None]).max(axis=2).max(axis=1)
+    to_alt = (np.abs(alts - dev[:, None]) / sig[:, None]).max(axis=2).min(axis=1)
     dof = nchan * nbin - (4 + nchan)
     dchi2 = (r["red_chi2"] - z["red_chi2"]) * dof
     near = dx <= 1e-3
-    print("config 3, %d subints: %d within 1e-3 sigma of the reference (max %.3g); reference "
-          "one-ulp floor > 1e-3 sigma on %d (max %.3g); |dchi2| max %.2e; nfev equal on %d" % (
-              nsub, near.sum(), dx.max(), (floor > 1e-3).sum(), floor.max(),
-              np.abs(dchi2).max(), (r["nfev"] == z["nfev"]).sum()))
+    on_alt = to_alt <= 1e-3
+    within = dx <= 1e-3 + 1.05 * spread
+    dn = r["nfev"] - z["nfev"].astype(int)
+    print("config 3, %d subints: %d within 1e-3 sigma of the reference (max %.3g), %d more on "
+          "one of the reference's own end points, %d between them; reference's own spread > "
+          "1e-3 sigma on %d (max %.3g); |dchi2| max %.2e; nfev equal on %d, max |dnfev| %d" % (
+              nsub, near.sum(), dx.max(), (on_alt & ~near).sum(), (~near & ~on_alt).sum(),
+              (spread > 1e-3).sum(), spread.max(), np.abs(dchi2).max(), (dn == 0).sum(),
+              np.abs(dn).max()))
     for i in np.where(~near)[0]:
-        print("   subint %3d: |dx|/sigma %.3g, reference floor %.3g, nfev %d (reference %d), "
-              "dchi2 %.2e" % (i, dx[i], floor[i], r["nfev"][i], z["nfev"][i], dchi2[i]))
+        print("   subint %3d: |dx|/sigma %.3g, to nearest reference end point %.3g, reference "
+              "spread %.3g, nfev %d (reference %d), dchi2 %.2e" % (
+                  i, dx[i], to_alt[i], spread[i], r["nfev"][i], z["nfev"][i], dchi2[i]))
     assert np.abs(dchi2).max() <= 1e-3
-    assert near.mean() >= 0.85
+    assert np.abs(dn).max() <= 2, np.where(np.abs(dn) > 2)
+    assert (near | on_alt | within).all(), np.where(~(near | on_alt | within))
+    stable = spread <= 1e-3
+    assert near[stable].all(), np.where(stable & ~near)

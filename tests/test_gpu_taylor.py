@@ -13,11 +13,11 @@ the moments moves the stopping point by up to a few 1e-4 sigma (seen: 2e-4
 sigma on 2 of 6 subints at 16 x 256 when the moment sweep was split into two
 accumulator chains).
 
-nfev is compared only in aggregate: with gtol = -1 trust-ncg stops when the
-predicted reduction rounds to <= 0, and on some subints both paths (and the
-CPU oracle) spend a different number of terminal, noise-driven shrink steps
-there (seen: 21 vs 6 evaluations, equal objective to 1e-16, params 5e-5
-sigma apart).  Most subints take the identical path.
+nfev is counted as scipy counts it (a proposal that repeats the last
+evaluated point is memoised, not re-evaluated) and compared within two:
+with gtol = -1 trust-ncg stops when the predicted reduction rounds to <= 0,
+and the last accept / reject decisions before that are taken on differences
+at the objective's rounding, where the two paths' sums differ.
 """
 import numpy as np
 import pytest
@@ -65,7 +65,7 @@ def _statuses_agree(t, e):
 
 def _assert_close(t, e, flags, tol=1e-3):
     _statuses_agree(t, e)
-    assert np.mean(t["nfev"] == e["nfev"]) >= 0.5, (t["nfev"], e["nfev"])
+    assert np.abs(t["nfev"] - e["nfev"]).max() <= 2, (t["nfev"], e["nfev"])
     for i in range(5):
         if flags[i]:
             sig = e["param_errs"][:, i]
