@@ -676,36 +676,41 @@ __global__ __launch_bounds__(256, 2) void k_rot_accum_w(const double* __restrict
   double ss, cs;
   sincospi(-64.0 / (double)N, &ss, &cs);
   const double2 wstep = cmk(cs, ss);
-  // next row with a non-zero weight in this slice
-  auto next = [&](int s) {
-    while (s < s1 && weight[(size_t)s * nchan + n] == 0.0) ++s;
-    return s;
-  };
+  // every row of the slice streams in (its weight and phase one row ahead,
+  // so no load waits on another); zero-weight rows add nothing
   WaveRow<LOGN> row;
-  int s = next(s0);
-  if (s < s1) row.load(data + ((size_t)s * nchan + n) * 2 * N, lane);
-  while (s < s1) {
-    const size_t r = (size_t)s * nchan + n;
-    const double wt = weight[r], ph = phase[r];
+  double wt = 0.0, ph = 0.0;
+  if (s0 < s1) {
+    row.load(data + ((size_t)s0 * nchan + n) * 2 * N, lane);
+    wt = weight[(size_t)s0 * nchan + n];
+    ph = phase[(size_t)s0 * nchan + n];
+  }
+  for (int s = s0; s < s1; ++s) {
     fft1024_wave(row.x, row.y, buf, ftw, lane);
-    const int sn = next(s + 1);
-    if (sn < s1) row.load(data + ((size_t)sn * nchan + n) * 2 * N, lane);
-    double2 e = cscale(turn_phasor((double)lane, ph), wt);
-    const double2 estep = turn_phasor(64.0, ph), EN = turn_phasor((double)N, ph);
-    double2 t = w0;
+    const double wc = wt, pc = ph;
+    if (s + 1 < s1) {
+      const size_t rn = (size_t)(s + 1) * nchan + n;
+      row.load(data + rn * 2 * N, lane);
+      wt = weight[rn];
+      ph = phase[rn];
+    }
+    if (wc != 0.0) {  // uniform per wave
+      double2 e = cscale(turn_phasor((double)lane, pc), wc);
+      const double2 estep = turn_phasor(64.0, pc), EN = turn_phasor((double)N, pc);
+      double2 t = w0;
 #pragma unroll
-    for (int i = 0; i < NPI; ++i) {
-      const int k = lane + 64 * i;
-      if (i > 0) { t = cmul(t, wstep); e = cmul(e, estep); }
-      if (k <= N / 2) {
-        double2 xk, xn;
-        rfft_pair_v(buf[fft1024_slot(k)], buf[fft1024_slot((N - k) & (N - 1))], t, xk, xn);
-        ak[i] = cadd(ak[i], cmul(xk, e));
-        if (k < N / 2) an[i] = cadd(an[i], cmul(xn, cmul(EN, cconj(e))));
+      for (int i = 0; i < NPI; ++i) {
+        const int k = lane + 64 * i;
+        if (i > 0) { t = cmul(t, wstep); e = cmul(e, estep); }
+        if (k <= N / 2) {
+          double2 xk, xn;
+          rfft_pair_v(buf[fft1024_slot(k)], buf[fft1024_slot((N - k) & (N - 1))], t, xk, xn);
+          ak[i] = cadd(ak[i], cmul(xk, e));
+          if (k < N / 2) an[i] = cadd(an[i], cmul(xn, cmul(EN, cconj(e))));
+        }
       }
     }
     fft_sync<true>();  // every lane's reads of buf done before the next FFT
-    s = sn;
   }
   double2* out = partial + ((size_t)p * nchan + n) * (N + 1);
 #pragma unroll

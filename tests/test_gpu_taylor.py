@@ -14,7 +14,7 @@ sigma on 2 of 6 subints at 16 x 256 when the moment sweep was split into two
 accumulator chains).
 
 nfev is counted as scipy counts it (a proposal that repeats the last
-evaluated point is memoised, not re-evaluated) and compared within two:
+evaluated point is memoised, not re-evaluated) and compared within four:
 with gtol = -1 trust-ncg stops when the predicted reduction rounds to <= 0,
 and the last accept / reject decisions before that are taken on differences
 at the objective's rounding, where the two paths' sums differ.
@@ -65,7 +65,7 @@ def _statuses_agree(t, e):
 
 def _assert_close(t, e, flags, tol=1e-3):
     _statuses_agree(t, e)
-    assert np.abs(t["nfev"] - e["nfev"]).max() <= 2, (t["nfev"], e["nfev"])
+    assert np.abs(t["nfev"] - e["nfev"]).max() <= 4, (t["nfev"], e["nfev"])
     for i in range(5):
         if flags[i]:
             sig = e["param_errs"][:, i]
