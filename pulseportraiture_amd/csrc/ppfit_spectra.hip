@@ -134,7 +134,12 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
   const double* drow0 = a.data + (size_t)s * nchan * (2 * N);
   double2* buf = bufs[w];
   auto active_g = [&](int q) { return q < nchan && (!mask || mask[q]); };
-  auto active = [&](int q) { return q < nchan && cact[q]; };  // after the cmeta barrier
+  // after the cmeta barrier; wave-uniform (q is), read as a scalar so that
+  // no branch on it is divergent in the compiler's view (a divergent join
+  // makes the wait-count pass drain every outstanding load and X store)
+  auto active = [&](int q) {
+    return q < nchan && __builtin_amdgcn_readfirstlane((int)cact[q]) != 0;
+  };
 
   WaveRow<LOGN> row;
   bool have = active_g(w);  // the registers hold (or are loading) this wave's next row
@@ -270,7 +275,10 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
             buf[bi(k)] = tk;
           }
         }
-        if (FULL) mload(i + 2, mk, mn);
+        // reload for iteration i + 2 only if there is one: a trailing load
+        // left in flight past the loop would be drained (with every X store
+        // issued before it) when the registers are reused for the next row
+        if (FULL && i + 2 < NPI) mload(i + 2, mk, mn);
       };
       static_assert(64 * (NPI - 1) <= N / 2 && 64 * (NPI - 1) + 63 >= N / 2, "pair split");
       constexpr int NFULL2 = (NPI - 1) & ~1;
@@ -306,13 +314,22 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
     if (a.guess) {
       __syncthreads();  // the group's rotated rows are complete
       if constexpr (RREG) {
+        // branch-free: each sum is selected, not skipped (the same additions
+        // in the same order as the guarded form)
+        int actv[WPB];
+#pragma unroll
+        for (int v = 0; v < WPB; ++v) actv[v] = __builtin_amdgcn_readfirstlane(s_act[v]);
 #pragma unroll
         for (int q = 0; q < Cfg::NRQ; ++q) {
           const int k = tid + nthr * q;
-          if (k <= N)
+          const bool kin = k <= N;
+          const int kk = kin ? k : N;
 #pragma unroll
-            for (int v = 0; v < WPB; ++v)
-              if (s_act[v]) rq[q] = cadd(rq[q], bufs[v][bi(k)]);
+          for (int v = 0; v < WPB; ++v) {
+            const double2 sum = cadd(rq[q], bufs[v][bi(kk)]);
+            const bool use = kin && actv[v];
+            rq[q] = cmk(use ? sum.x : rq[q].x, use ? sum.y : rq[q].y);
+          }
         }
       } else {
         if (s_act[0])

@@ -271,32 +271,43 @@ class _UnitStack:
 
     def fit_and_accumulate(self, eng, model_port, fit_dm, accum, tw, mark=None):
         """One iteration's fits (ppalign.py:178-195) and weighted rotate-and-sum
-        (ppalign.py:202-208) in the Fourier domain."""
+        (ppalign.py:202-208) in the Fourier domain.  The fit results stay on
+        the device: the rotation phases and weights are formed there and fed
+        to the rotate-and-sum without a host round trip."""
         import time
         t0 = time.perf_counter()
         n = self.n
         init = np.stack([np.zeros(n), self.DMg, np.zeros(n), np.zeros(n), np.zeros(n)], 1)
         flags = [1, int(bool(fit_dm)), 0, 0, 0]
-        res = fit_portraits_batch(self.pols[0], model_port, init, self.P, self.freqs,
+        out = fit_portraits_batch(self.pols[0], model_port, init, self.P, self.freqs,
                                   nu_fits=np.stack([self.nu_fit] * 3, 1), errs=self.errs,
                                   fit_flags=flags, log10_tau=False, chan_mask=self.mask,
                                   weights=self.wts, guess=True, guess_Ns=model_port.shape[1],
-                                  guess_wrap=False, guess_nu=self.nu_fit)
+                                  guess_wrap=False, guess_nu=self.nu_fit, to_host=False)
         if mark is not None:
             t0 = mark("fit", t0)
-        phase = res["params"][:, 0]
-        DM = res["params"][:, 1]
-        nu_ref = res["nu_out"][:, 0]
+        dev = eng.device
+        out = {k: torch.as_tensor(out[k], device=dev) for k in ("params", "nu_out", "scales")}
+        if getattr(self, "_dv", None) is None:  # per-unit constants, once
+            f64 = dict(dtype=torch.float64, device=dev)
+            self._dv = dict(P=torch.as_tensor(self.P, **f64),
+                            f2=torch.as_tensor(self.freqs ** -2.0, **f64),
+                            e2=torch.as_tensor(self.errs ** 2, **f64),
+                            on=torch.as_tensor(self.mask > 0, device=dev))
+        dv = self._dv
+        phase = out["params"][:, 0]
+        DM = out["params"][:, 1]
+        nu_ref = out["nu_out"][:, 0]
         # rotate_data(port, phase, DM, P, freqs, nu_ref) per channel (pplib.py:2406-2415)
-        ph = phase[:, None] + (Dconst * DM / self.P)[:, None] * \
-            (self.freqs ** -2.0 - nu_ref[:, None] ** -2.0)
-        w = np.where(self.mask > 0, res["scales"] / self.errs ** 2, 0.0)
+        ph = phase[:, None] + (Dconst * DM / dv["P"])[:, None] * (dv["f2"] - nu_ref[:, None] ** -2.0)
+        w = torch.where(dv["on"], out["scales"] / dv["e2"], torch.zeros((), dtype=torch.float64,
+                                                                       device=dev))
         for ipol, pol in enumerate(self.pols):
             eng.rotate_accumulate(pol, ph, w, accum[ipol])
-        tw += torch.as_tensor(w.sum(axis=0), device=tw.device)
+        tw += w.sum(dim=0).to(tw.device)
         if mark is not None:
             mark("accumulate", t0)
-        return res
+        return out
 
 
 def align_archives(metafile, initial_guess, fit_dm=True, tscrunch=False, pscrunch=True,
@@ -372,13 +383,15 @@ def align_archives(metafile, initial_guess, fit_dm=True, tscrunch=False, pscrunc
         allreduce_sum(accum, tw)
         spec = torch.view_as_complex(accum).reshape(npol * nchan, nharm)
         port = eng.irfft_rows(spec, nbin).reshape(npol, nchan, nbin)
-        good = tw > 0
-        port[:, good] = port[:, good] / tw[good][None, :, None]
-        aligned = port.cpu().numpy()
-        model_port = aligned[0]
+        good = (tw > 0)[None, :, None]
+        port = torch.where(good, port / tw[None, :, None], port)
+        # the next iteration's template stays on the device (the 1-channel
+        # hack and the caller take it on the host)
+        model_port = port[0].cpu().numpy() if single else port[0]
         t0 = mark("exchange", t0)
         niter -= 1
         count += 1
+    aligned = port.cpu().numpy()
     if norm in ("mean", "max", "prof", "rms", "abs"):
         from .pplib import get_noise
         for ipol in range(npol):
