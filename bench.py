@@ -299,11 +299,15 @@ def leg_ppalign(eng, narch, niter, seed):
     # warm-up: the same call at niter 1 (device workspace and the caching
     # allocator reach their steady-state sizes outside the timed call)
     ppalign.align_archives(names, "bench_pa_guess", niter=1, quiet=True)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    port = ppalign.align_archives(names, "bench_pa_guess", fit_dm=True, niter=niter, quiet=True)
-    torch.cuda.synchronize()
-    t = time.perf_counter() - t0
+    calls = []
+    for _ in range(2):  # the reported time is the faster of two timed calls
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        port = ppalign.align_archives(names, "bench_pa_guess", fit_dm=True, niter=niter,
+                                      quiet=True)
+        torch.cuda.synchronize()
+        calls.append(time.perf_counter() - t0)
+    t = min(calls)
     # the same call again with a synchronisation at every phase boundary
     # (diagnostic split of the time above; not the timed call)
     phases = {}
@@ -313,7 +317,8 @@ def leg_ppalign(eng, narch, niter, seed):
         archive.unregister_archive(nm)
     del data
     return {"value": round(narch * niter / t, 1), "unit": "archive-iterations/s",
-            "s_per_call": round(t, 3), "narch": narch, "niter": niter,
+            "s_per_call": round(t, 3), "s_per_call_each": [round(c, 3) for c in calls],
+            "narch": narch, "niter": niter,
             "ms_per_iteration": round(t / niter * 1e3, 2),
             "data_gb": round(narch * nchan * nbin * 8 / 1e9, 2),
             "template_finite": bool(np.isfinite(port).all()),

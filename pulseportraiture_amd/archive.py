@@ -133,7 +133,10 @@ class _Registered:
         self.base = _registry[name]
 
     def meta(self):
-        return DataBunch(**{k: v for k, v in self.base.items() if k != "subints"})
+        b = DataBunch()
+        b.update(self.base)  # shallow copy (C-level), then drop the data
+        b.pop("subints", None)
+        return b
 
     def read(self, lo, hi):
         return self.base.subints[lo:hi]
@@ -295,7 +298,8 @@ class Archive:
             self.rot_sign, dmc = -1.0, 0
         self.rm_base = bool(rm_baseline) and not raw.get("baseline_removed", True)
         self.tscrunch = bool(tscrunch) and raw.nsub > 1
-        m = DataBunch(**dict(raw))
+        m = DataBunch()
+        m.update(raw)
         m.dmc = dmc
         m.baseline_removed = bool(raw.get("baseline_removed", True) or rm_baseline)
         if self.tscrunch:

@@ -972,7 +972,9 @@ __device__ void guess_subint(const FitArgs& a, int c, int s, unsigned char* dyn,
     // modelx.mean(axis=0) over the fitted channels (pptoas.py:454); its
     // spectrum is the mean of the DC-zeroed channel spectra.
     double2 mm = cmk(0.0, 0.0);
-    if (!mask && a.Mmean) {
+    // every channel fitted: the mean template spectrum of k_model_mean (the
+    // same sum in the same order, scaled by 1 / nchan as 1 / cnt)
+    if ((!mask || cnt == (double)nchan) && a.Mmean) {
       mm = a.Mmean[(size_t)midx * a.NHP + k];
     } else {
       for (int n = 0; n < nchan; ++n)

@@ -277,24 +277,31 @@ class _UnitStack:
         import time
         t0 = time.perf_counter()
         n = self.n
-        init = np.stack([np.zeros(n), self.DMg, np.zeros(n), np.zeros(n), np.zeros(n)], 1)
-        flags = [1, int(bool(fit_dm)), 0, 0, 0]
-        out = fit_portraits_batch(self.pols[0], model_port, init, self.P, self.freqs,
-                                  nu_fits=np.stack([self.nu_fit] * 3, 1), errs=self.errs,
-                                  fit_flags=flags, log10_tau=False, chan_mask=self.mask,
-                                  weights=self.wts, guess=True, guess_Ns=model_port.shape[1],
-                                  guess_wrap=False, guess_nu=self.nu_fit, to_host=False)
-        if mark is not None:
-            t0 = mark("fit", t0)
         dev = eng.device
-        out = {k: torch.as_tensor(out[k], device=dev) for k in ("params", "nu_out", "scales")}
-        if getattr(self, "_dv", None) is None:  # per-unit constants, once
+        if getattr(self, "_dv", None) is None:  # per-unit inputs, on the device once
             f64 = dict(dtype=torch.float64, device=dev)
+            init = np.stack([np.zeros(n), self.DMg, np.zeros(n), np.zeros(n), np.zeros(n)], 1)
             self._dv = dict(P=torch.as_tensor(self.P, **f64),
                             f2=torch.as_tensor(self.freqs ** -2.0, **f64),
                             e2=torch.as_tensor(self.errs ** 2, **f64),
-                            on=torch.as_tensor(self.mask > 0, device=dev))
+                            on=torch.as_tensor(self.mask > 0, device=dev),
+                            init=torch.as_tensor(init, **f64),
+                            freqs=torch.as_tensor(self.freqs, **f64),
+                            errs=torch.as_tensor(self.errs, **f64),
+                            mask=torch.as_tensor(self.mask, device=dev),
+                            wts=torch.as_tensor(self.wts, **f64),
+                            nu3=torch.as_tensor(np.stack([self.nu_fit] * 3, 1), **f64),
+                            nu=torch.as_tensor(self.nu_fit, **f64))
         dv = self._dv
+        flags = [1, int(bool(fit_dm)), 0, 0, 0]
+        out = fit_portraits_batch(self.pols[0], model_port, dv["init"], dv["P"], dv["freqs"],
+                                  nu_fits=dv["nu3"], errs=dv["errs"], fit_flags=flags,
+                                  log10_tau=False, chan_mask=dv["mask"], weights=dv["wts"],
+                                  guess=True, guess_Ns=model_port.shape[1], guess_wrap=False,
+                                  guess_nu=dv["nu"], to_host=False)
+        if mark is not None:
+            t0 = mark("fit", t0)
+        out = {k: torch.as_tensor(out[k], device=dev) for k in ("params", "nu_out", "scales")}
         phase = out["params"][:, 0]
         DM = out["params"][:, 1]
         nu_ref = out["nu_out"][:, 0]
