@@ -59,9 +59,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 FP64_PEAK_TFLOPS = 78.6  # AMD MI355X spec, fp64 vector = fp64 matrix (not in the guide's table)
 # HBM bytes per launch per kernel from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
 # passes over this same bench (tools/profile_r03.sh + tools/pmc_summary.py)
-PMC_TRAFFIC = {"headline": os.path.join(ROOT, "profiles", "r03_pmc_traffic_headline.json"),
-               "scattering": os.path.join(ROOT, "profiles", "r03_pmc_traffic_scattering.json")}
+PMC_TRAFFIC = {c: os.path.join(ROOT, "profiles", "r04_pmc_traffic_%s.json" % c)
+               for c in ("headline", "scattering", "gm", "ppalign")}
 KERNEL_SYMBOL = {"solve": "k_scat_sweep", "data_xspec": "k_data_xspec<10>",
+                 "rot_accum": "k_rot_accum_w",
                  "post": "k_post<false>", "guess": "k_guess_w", "moments": "k_moments<4>",
                  "fit_taylor": "k_fit_taylor<true>"}
 # fp64 operations of one scattering cell evaluation as cells_scat forms them
@@ -308,11 +309,17 @@ def leg_ppalign(eng, narch, niter, seed):
         torch.cuda.synchronize()
         calls.append(time.perf_counter() - t0)
     t = min(calls)
-    # the same call again with a synchronisation at every phase boundary
-    # (diagnostic split of the time above; not the timed call)
+    # the same call again with a synchronisation at every phase boundary and
+    # HIP events around every kernel launch (diagnostic split of the time
+    # above, and the roofline's kernel times; not the timed call)
     phases = {}
+    eng.set_timing(True)
+    eng.reset_kernel_times()
     ppalign.align_archives(names, "bench_pa_guess", fit_dm=True, niter=niter, quiet=True,
                            timings=phases)
+    ktimes = {k: eng.kernel_time(k) for k in ("data_xspec", "rot_accum", "guess", "fit_taylor",
+                                              "post", "noise", "irfft")}
+    eng.set_timing(False)
     for nm in names + ["bench_pa_guess"]:
         archive.unregister_archive(nm)
     del data
@@ -323,6 +330,9 @@ def leg_ppalign(eng, narch, niter, seed):
             "data_gb": round(narch * nchan * nbin * 8 / 1e9, 2),
             "template_finite": bool(np.isfinite(port).all()),
             "phase_s": {k: round(v, 4) for k, v in phases.items() if k != "start"},
+            "kernel_ms_per_iteration": {k: round(v[0] / niter, 4) for k, v in ktimes.items()},
+            "kernel_launches": {k: v[1] for k, v in ktimes.items()},
+            "_ktimes": ktimes,
             "workload": "config 5: %d archives x 1 subint x %d chan x %d bin, fit_dm, niter %d; "
                         "setup (registration, unit stack) inside the timed call"
                         % (narch, nchan, nbin, niter)}
@@ -498,6 +508,7 @@ def main():
         legs["get_toas"] = g
         legs["get_toas_host"], _ = leg_get_toas(eng, w, data, reps=1, host=True)
         legs["ppalign"] = leg_ppalign(eng, args.ppalign_narch, args.ppalign_niter, args.seed)
+        legs["ppalign"].pop("_ktimes", None)
 
     if rank != 0:
         if world > 1:
@@ -674,6 +685,39 @@ def main_ppalign(args, eng, rank, world):
                          "units and all-reduces when torch.distributed is initialised")
     narch = args.nsub or args.ppalign_narch
     r = leg_ppalign(eng, narch, args.ppalign_niter, args.seed)
+    kt = r.pop("_ktimes")
+    nchan, nbin = 256, 2048
+    nharm = nbin // 2 + 1
+    # per launch (one launch per iteration each): the data pass reads every
+    # sample and writes X; the rotate-and-sum reads every sample again
+    model = {"data_xspec": (narch * (8.0 * nchan * nbin + 16.0 * nchan * nharm),
+                            "k_data_xspec: 8 B/sample read + 16 B/cell X written"),
+             "rot_accum": (narch * 8.0 * nchan * nbin,
+                           "k_rot_accum_w: 8 B/sample read (rotate-and-sum, ppalign.py:202-208)"),
+             "fit_taylor": (narch * 16.0 * nchan * nharm,
+                            "k_fit_taylor<true>: 16 B/cell X read (moment pass)")}
+    kernels = {}
+    niter = args.ppalign_niter
+    for k, (b, what) in model.items():
+        ms, n = kt[k]
+        if not n:
+            continue
+        # one pass per iteration (rot_accum's timed launches also count its
+        # small partial-sum reduction)
+        avg = ms / niter / 1e3
+        tr = pmc_traffic(k, narch, "ppalign")
+        kernels[k] = {"bound": "hbm", "achieved": round(b / avg / 1e9, 1), "peak": HBM_PEAK_GBS,
+                      "unit": "GB/s", "frac": round(b / avg / 1e9 / HBM_PEAK_GBS, 4),
+                      "traffic": tr, "algorithmic_bytes_per_launch": b,
+                      "avg_launch_ms": round(avg * 1e3, 4), "bytes_model": what}
+    dom = max(kernels, key=lambda k: kernels[k]["avg_launch_ms"]) if kernels else None
+    roof = None
+    if dom:
+        roof = dict(kernel=dom, **kernels[dom])
+        roof["traffic_unit"] = "bytes/launch"
+        src = PMC_TRAFFIC["ppalign"]
+        roof["traffic_source"] = os.path.relpath(src, ROOT) if roof["traffic"] else None
+        roof["other_kernels"] = {k: v for k, v in kernels.items() if k != dom}
     line = {"metric": "archive-iterations/sec (ppalign.align_archives, 256ch×2048bin fp64)",
             "value": r["value"], "unit": r["unit"], "n_gpus": 1, "steps": 1, "warmup": 1,
             "ms_per_step": round(r["s_per_call"] * 1e3, 2), "higher_is_better": True,
@@ -682,7 +726,7 @@ def main_ppalign(args, eng, rank, world):
                     "noise; generated on device)",
             "config": {"workload": r["workload"], "narch": narch, "nchan": 256, "nbin": 2048,
                        "niter": args.ppalign_niter, "parallelism": "dp1"},
-            "detail": r, "roofline": None, "cpu_baseline": None}
+            "detail": r, "roofline": roof, "cpu_baseline": None}
     print(json.dumps(line))
 
 

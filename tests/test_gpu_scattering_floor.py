@@ -8,12 +8,12 @@ through the SURVEY §8(c) shim):
   errors, status, nfev, red chi2, and four restarts one ulp away in phase
   and log10 tau;
 * scattering_200_perm.npz (make_golden_cfg3_perm.py): the same fits with the
-  channels in 8 seeded random orders -- every per-channel term the same
+  channels in 24 seeded random orders -- every per-channel term the same
   number, only the order of the reference's own channel sums changed.
 
 trust-ncg with gtol = -1 (pptoaslib.py:1002) stops at the first predicted
 reduction <= 0, i.e. when its trust radius has collapsed onto rounding; on
-42 of these 200 subints the reference itself ends more than 1e-3 sigma away
+45 of these 200 subints the reference itself ends more than 1e-3 sigma away
 from its own answer under a reordering of its sums (up to 46 sigma in phi: the
 end points differ by ~1e-2 sigma in DM, tau, alpha, and the zero-covariance
 frequency nu_DM the phase is reported at moves with them).  Those end points
