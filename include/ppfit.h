@@ -228,6 +228,12 @@ typedef struct {
                            (legacy pplib.fit_portrait errors, pplib.py:2184-2190) */
   double* grad;         /* [nsub][5] or NULL: gradient at the final point (jac) */
   double* hess;         /* [nsub][5][5] or NULL: Hessian at the final point     */
+  double* errs_out;     /* [nsub][nchan] or NULL: the time-domain noise sigma
+                           each channel was fitted with -- desc->errs, or
+                           get_noise_PS of the row where that is NULL / NaN
+                           (pplib.py:2227-2253); 0 for masked channels.  Lets
+                           a caller weight by load_data's noise_stds without
+                           a separate noise pass (ppalign.py:202-208)      */
 } ppf_fit_result;
 
 int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* desc,

@@ -54,7 +54,7 @@ class FitResult(ctypes.Structure):
                 ("channel_snrs", _dp), ("chi2", _dp), ("red_chi2", _dp),
                 ("snr", _dp), ("nfev", _dp), ("status", _dp),
                 ("init_used", _dp), ("fun", _dp), ("cov_nosc", _dp),
-                ("grad", _dp), ("hess", _dp)]
+                ("grad", _dp), ("hess", _dp), ("errs_out", _dp)]
 
 
 EXPORTS = {

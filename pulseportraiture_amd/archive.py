@@ -286,6 +286,8 @@ class Archive:
             self.owns_reads = bool(getattr(src, "owns_reads", True))
         finally:
             src.close()
+        # a registered source holds no file: keep it for the reads
+        self._reg = src if isinstance(src, _Registered) else None
         if not isinstance(filename, str):
             filename = raw.get("filename", "archive")
         raw.setdefault("filename", filename)
@@ -313,6 +315,8 @@ class Archive:
         return self.meta.nsub
 
     def _read_src(self, lo, hi):
+        if self._reg is not None:
+            return self._reg.read(lo, hi)
         src = _source(*self._src_args)
         try:
             return src.read(lo, hi)

@@ -612,6 +612,10 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
               hipLaunchKernelGGL(k_post<false>, dim3(n), dim3(kBlock), lds_meta, st, fp);
             }))
           return r;
+        if (o->errs_out)
+          HIPCHK(ctx, hipMemcpyAsync(o->errs_out + (size_t)(s0 + off) * nchan, sp.sig,
+                                     (size_t)n * nchan * sizeof(double),
+                                     hipMemcpyDeviceToDevice, st));
       }
     }
     // join: the caller's stream sees every piece
@@ -754,6 +758,10 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
           hipLaunchKernelGGL(k_post<true>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
         }))
       return r;
+    if (o->errs_out)  // the sigma each channel was fitted with (k_data_xspec)
+      HIPCHK(ctx, hipMemcpyAsync(o->errs_out + (size_t)s0 * nchan, sa.sig,
+                                 (size_t)nc * nchan * sizeof(double), hipMemcpyDeviceToDevice,
+                                 ctx->stream));
   }
   return PPF_OK;
 }
@@ -1071,10 +1079,12 @@ int ppf_rotate_accumulate(ppf_ctx* ctx, int32_t nsub, int32_t nchan, int32_t nbi
   const double2* tw;
   if (int r = twiddles(ctx, nbin, &tw)) return r;
   const int NH = nbin / 2 + 1;
-  // nbin 2048: one wave per row (register FFT), workgroups of four channels,
-  // about 8 waves per SIMD; else one workgroup per (slice, channel)
+  // one workgroup per (slice, channel), about 2048 of them (8 per CU); nbin
+  // 2048: four waves each streaming every fourth row of the slice (register
+  // FFT), so a slice should hold a few groups of four
   const bool wave = logN == 10;
-  int nsplit = wave ? (8192 + nchan - 1) / nchan : (2048 + nchan - 1) / nchan;
+  int nsplit = (2048 + nchan - 1) / nchan;
+  if (wave && nsplit > (nsub + 3) / 4) nsplit = (nsub + 3) / 4;
   if (nsplit > nsub) nsplit = nsub;
   if (nsplit < 1) nsplit = 1;
   const size_t count = (size_t)nchan * NH;
@@ -1082,7 +1092,7 @@ int ppf_rotate_accumulate(ppf_ctx* ctx, int32_t nsub, int32_t nchan, int32_t nbi
   double2* partial = reinterpret_cast<double2*>(ctx->aux.p);
   if (int r = timed(ctx, PPF_K_ROT_ACCUM, [&] {
         if (wave)
-          hipLaunchKernelGGL(k_rot_accum_w, dim3(nsplit * ((nchan + 3) / 4)), dim3(256), 0,
+          hipLaunchKernelGGL(k_rot_accum_w, dim3(nsplit * nchan), dim3(256), 0,
                              ctx->stream, data, phase, weight, partial, nsub, nchan, nsplit, tw);
         else
           LOGN_SWITCH(logN, hipLaunchKernelGGL(k_rot_accum<LG>, dim3(nsplit * nchan),

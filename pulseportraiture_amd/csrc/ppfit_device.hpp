@@ -11,6 +11,11 @@
 // moment pass's X loads were slower with the hint and stay plain)
 #define PPF_NT 1
 #endif
+#ifndef PPF_EARLY_ROW
+// wave-per-row streams (data pass, ppalign's rotate-and-sum) start the next
+// row's load inside the register FFT, right after stage A (A/B knob)
+#define PPF_EARLY_ROW 1
+#endif
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <type_traits>
@@ -151,6 +156,14 @@ __device__ __forceinline__ double lane_at(double v) {
   const unsigned long long u = __double_as_longlong(v);
   const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, J);
   const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), J);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// Lane j's value (j wave-uniform, known at run time), wave-uniform.
+__device__ __forceinline__ double lane_of(double v, int j) {
+  const unsigned long long u = __double_as_longlong(v);
+  const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, j);
+  const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), j);
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
@@ -666,9 +679,18 @@ constexpr int kFftPadRow = 68;                // stage-A transpose row pitch
 constexpr int kFft1024Slots = 16 * kFftPadRow;  // >= P(1024) + 1
 __device__ __forceinline__ int fft1024_slot(int k) { return k + ((k >> 8) << 2); }
 
+struct NoHook {
+  __device__ __forceinline__ void operator()() const {}
+};
+
 // row: x[m], y[m] = packed sample j + 64 m of this lane (WaveRow<10>).
+// after_a runs once stage A has left the row in LDS: the row registers are
+// free from there, so a caller can start the next row's load in it and have
+// stages B and C (not only its own post-processing) cover that load.
+template <class Hook = NoHook>
 __device__ __forceinline__ void fft1024_wave(const double (&x)[16], const double (&y)[16],
-                                             double2* buf, const Fft1024Tw& t, int lane) {
+                                             double2* buf, const Fft1024Tw& t, int lane,
+                                             Hook after_a = Hook{}) {
   double2 v[16];
 #pragma unroll
   for (int m = 0; m < 16; ++m) v[m] = cmk(x[m], y[m]);
@@ -680,6 +702,7 @@ __device__ __forceinline__ void fft1024_wave(const double (&x)[16], const double
 #pragma unroll
   for (int r = 0; r < 16; ++r)
     buf[r * kFftPadRow + lane] = r ? cmul(v[dft16_pos(r)], tw_pow(r, lo, hi)) : v[0];
+  after_a();
   fft_sync<true>();
   const int j0 = lane & 3, rr = lane >> 2;
 #pragma unroll

@@ -212,22 +212,28 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
       mn = Mr[N - k];
     };
     double2 m0k = cmk(0.0, 0.0), m0n = m0k, m1k = m0k, m1n = m0k;
+    // next row of this wave: with the register FFT its load starts as soon
+    // as stage A has moved the current row to LDS (stages B, C and the
+    // spectrum pass cover it), else after the FFT
+    const bool nxt = active(n + WPB);
+    auto load_next = [&] {
+      if (nxt) row.load(drow0 + (size_t)(n + WPB) * 2 * N, lane);
+    };
+    constexpr bool EARLY = REGFFT && PPF_EARLY_ROW;
     if (act) {
       mload(0, m0k, m0n);
       mload(1, m1k, m1n);
       if constexpr (REGFFT) {
-        fft1024_wave(row.x, row.y, buf, ftw[0], lane);
+        if constexpr (EARLY) fft1024_wave(row.x, row.y, buf, ftw[0], lane, load_next);
+        else fft1024_wave(row.x, row.y, buf, ftw[0], lane);
       } else {
         row.store(buf, drow0 + (size_t)n * 2 * N, lane);
         fft_sync<true>();
         wave_fft<LOGN>(buf, twl, lane);
       }
     }
-    // next row of this wave streams in during the spectrum pass
-    if (active(n + WPB)) {
-      row.load(drow0 + (size_t)(n + WPB) * 2 * N, lane);
-      have = true;
-    }
+    if (!EARLY || !act) load_next();
+    have = nxt;
     if (act) {
       const double2 cm = cmeta[n];
       const double wgt = cm.y;
@@ -657,82 +663,112 @@ __global__ __launch_bounds__(kBlock) void k_rot_accum(const double* __restrict__
   }
 }
 
-// The same sum for nbin = 2048 (ppalign at config 5): one wave per channel
-// row, as the data pass streams them (fft1024_wave, next row in flight in
-// registers).  Workgroup (g, p) takes channels 4 g .. 4 g + 3 of subint slice
-// p, so its four waves read adjacent rows; each lane keeps the harmonics
-// k = lane + 64 i and N - k (i <= 8) of its channel's sum in registers.  The
-// rotation e^{2 pi i k ph} w follows the data pass's guess phasor chain
-// (turn_phasor at lane, 64 and N, stepped per pair iteration).
+// The same sum for nbin = 2048 (ppalign at config 5).  Workgroup (n, p)
+// takes channel n of subint slice p; its four waves stream subints s0 + w,
+// s0 + w + 4, ... (one row per wave per group, fft1024_wave into the wave's
+// own LDS buffer, the next row's load started after stage A).  After a
+// barrier every wave adds all four rows of the group, in subint order, into
+// the harmonic pairs it owns: k = lane + 64 j and N - k for j = w, w + 4,
+// w + 8 (j <= 8).  Spreading the pairs over the workgroup keeps 6 complex
+// sums per lane instead of a whole channel spectrum (18), which spilled.
+// The rotation e^{2 pi i k ph} w: turn_phasor at k = lane + 64 w per row,
+// stepped by e^{2 pi i 256 ph}; the row's own wave forms that step and
+// e^{2 pi i N ph} once and passes them with the weight through LDS.
 __global__ __launch_bounds__(256, 2) void k_rot_accum_w(const double* __restrict__ data,
                                                        const double* __restrict__ phase,
                                                        const double* __restrict__ weight,
                                                        double2* __restrict__ partial, int nsub,
                                                        int nchan, int nsplit,
                                                        const double2* __restrict__ tw) {
-  constexpr int LOGN = 10, N = 1 << LOGN, NPI = (N / 2 + 1 + 63) / 64;
+  constexpr int LOGN = 10, N = 1 << LOGN, NJ = 3;  // j = w + 4 i <= 8
   __shared__ double2 bufs[4][kFft1024Slots];
   __shared__ Fft1024Tw ftw;
+  __shared__ double2 s_step[4], s_EN[4];
+  __shared__ double s_w[4], s_ph[4];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int ngrp = (nchan + 3) / 4;
-  const int g = blockIdx.x % ngrp, p = blockIdx.x / ngrp;
-  const int n = 4 * g + w;
+  const int n = blockIdx.x % nchan, p = blockIdx.x / nchan;
   const int per = (nsub + nsplit - 1) / nsplit;
   const int s0 = p * per, s1 = min(nsub, s0 + per);
+  const int ngrp = s1 > s0 ? (s1 - s0 + 3) / 4 : 0;
   ftw.fill(tw, tid, 256);
-  __syncthreads();
-  if (n >= nchan) return;  // no barriers below
   double2* buf = bufs[w];
-  double2 ak[NPI], an[NPI];
+  double2 ak[NJ], an[NJ], tk[NJ];
 #pragma unroll
-  for (int i = 0; i < NPI; ++i) ak[i] = an[i] = cmk(0.0, 0.0);
-  double sw, cw;
-  sincospi(-(double)lane / (double)N, &sw, &cw);
-  const double2 w0 = cmk(cw, sw);  // e^{-i pi lane / N}
-  double ss, cs;
-  sincospi(-64.0 / (double)N, &ss, &cs);
-  const double2 wstep = cmk(cs, ss);
-  // every row of the slice streams in (its weight and phase one row ahead,
-  // so no load waits on another); zero-weight rows add nothing
-  WaveRow<LOGN> row;
-  double wt = 0.0, ph = 0.0;
-  if (s0 < s1) {
-    row.load(data + ((size_t)s0 * nchan + n) * 2 * N, lane);
-    wt = weight[(size_t)s0 * nchan + n];
-    ph = phase[(size_t)s0 * nchan + n];
+  for (int i = 0; i < NJ; ++i) {
+    ak[i] = an[i] = cmk(0.0, 0.0);
+    double sw, cw;  // rfft post-processing twiddle e^{-i pi k / N} of pair k
+    sincospi(-(double)(lane + 64 * (w + 4 * i)) / (double)N, &sw, &cw);
+    tk[i] = cmk(cw, sw);
   }
-  for (int s = s0; s < s1; ++s) {
-    fft1024_wave(row.x, row.y, buf, ftw, lane);
-    const double wc = wt, pc = ph;
-    if (s + 1 < s1) {
-      const size_t rn = (size_t)(s + 1) * nchan + n;
-      row.load(data + rn * 2 * N, lane);
-      wt = weight[rn];
-      ph = phase[rn];
+  auto rowp = [&](int s) { return data + ((size_t)s * nchan + n) * 2 * N; };
+  // weights and phases of this wave's rows 64 groups at a time (lane l: group
+  // t0 + l), one window ahead, as vector loads: a scalar load per row would
+  // hold up the FFT's LDS waits (they share lgkmcnt)
+  auto wload = [&](int t0, double& wo, double& po) {
+    const int s = s0 + 4 * (t0 + lane) + w;
+    const size_t i = (size_t)(s < s1 ? s : s0) * nchan + n;
+    wo = weight[i];
+    po = phase[i];
+    if (s >= s1) wo = 0.0;
+  };
+  double wv = 0.0, pv = 0.0, wv2 = 0.0, pv2 = 0.0;
+  if (ngrp > 0) wload(0, wv2, pv2);
+  WaveRow<LOGN> row;
+  if (s0 + w < s1) row.load(rowp(s0 + w), lane);
+  __syncthreads();  // ftw
+  for (int t = 0; t < ngrp; ++t) {
+    const int sc = s0 + 4 * t + w, sn = sc + 4;  // this wave's row now and next
+    if ((t & 63) == 0) {
+      wv = wv2;
+      pv = pv2;
+      if (t + 64 < ngrp) wload(t + 64, wv2, pv2);
     }
-    if (wc != 0.0) {  // uniform per wave
-      double2 e = cscale(turn_phasor((double)lane, pc), wc);
-      const double2 estep = turn_phasor(64.0, pc), EN = turn_phasor((double)N, pc);
-      double2 t = w0;
+    const double wc = lane_of(wv, t & 63), pc = lane_of(pv, t & 63);  // 0 past s1
+    auto load_next = [&] {
+      if (sn < s1) row.load(rowp(sn), lane);
+    };
+    if (wc != 0.0) {
+      if constexpr (PPF_EARLY_ROW) {
+        fft1024_wave(row.x, row.y, buf, ftw, lane, load_next);
+      } else {
+        fft1024_wave(row.x, row.y, buf, ftw, lane);
+        load_next();
+      }
+      const double2 st = turn_phasor(256.0, pc), en = turn_phasor((double)N, pc);
+      if (lane == 0) { s_step[w] = st; s_EN[w] = en; s_ph[w] = pc; }
+    } else {
+      load_next();
+    }
+    if (lane == 0) s_w[w] = wc;
+    __syncthreads();  // the group's four spectra and their rotations
 #pragma unroll
-      for (int i = 0; i < NPI; ++i) {
-        const int k = lane + 64 * i;
-        if (i > 0) { t = cmul(t, wstep); e = cmul(e, estep); }
-        if (k <= N / 2) {
-          double2 xk, xn;
-          rfft_pair_v(buf[fft1024_slot(k)], buf[fft1024_slot((N - k) & (N - 1))], t, xk, xn);
-          ak[i] = cadd(ak[i], cmul(xk, e));
-          if (k < N / 2) an[i] = cadd(an[i], cmul(xn, cmul(EN, cconj(e))));
+    for (int r = 0; r < 4; ++r) {
+      const double wr = s_w[r];
+      if (wr != 0.0) {  // uniform per workgroup
+        const double pr = s_ph[r];
+        const double2 st = s_step[r], EN = s_EN[r];
+        const double2* br = bufs[r];
+        double2 e = cscale(turn_phasor((double)(lane + 64 * w), pr), wr);
+#pragma unroll
+        for (int i = 0; i < NJ; ++i) {
+          const int k = lane + 64 * (w + 4 * i);
+          if (i > 0) e = cmul(e, st);
+          if (k <= N / 2) {
+            double2 xk, xn;
+            rfft_pair_v(br[fft1024_slot(k)], br[fft1024_slot((N - k) & (N - 1))], tk[i], xk, xn);
+            ak[i] = cadd(ak[i], cmul(xk, e));
+            if (k < N / 2) an[i] = cadd(an[i], cmul(xn, cmul(EN, cconj(e))));
+          }
         }
       }
     }
-    fft_sync<true>();  // every lane's reads of buf done before the next FFT
+    __syncthreads();  // buffers and the row table free for the next group
   }
   double2* out = partial + ((size_t)p * nchan + n) * (N + 1);
 #pragma unroll
-  for (int i = 0; i < NPI; ++i) {
-    const int k = lane + 64 * i;
+  for (int i = 0; i < NJ; ++i) {
+    const int k = lane + 64 * (w + 4 * i);
     if (k <= N / 2) {
       out[k] = ak[i];
       if (k < N / 2) out[N - k] = an[i];  // k = 0: the Nyquist harmonic

@@ -192,7 +192,8 @@ class Engine:
         bounds: 5 (low, high) pairs, None = unbounded (TNC only).
         eval_only: f, g, H and the post-fit at init, no solver step.
         guess_direct: brute-force guess grid by direct sums (no folded DFT).
-        Returns a dict of device tensors.
+        Returns a dict of device tensors ("errs": the per-channel noise sigma
+        each channel was fitted with, 0 for masked channels).
         """
         if method not in _lib.METHODS:
             raise PPFitError("Method '%s' is not implemented." % method)
@@ -260,12 +261,14 @@ class Engine:
                    fun=torch.empty(nsub, **f64),
                    cov_nosc=torch.empty(nsub, 5, 5, **f64),
                    grad=torch.empty(nsub, 5, **f64),
-                   hess=torch.empty(nsub, 5, 5, **f64))
+                   hess=torch.empty(nsub, 5, 5, **f64),
+                   errs=torch.empty(nsub, nchan, **f64))
         res = _lib.FitResult()
         for k in ["params", "param_errs", "nu_out", "cov", "scales", "scale_errs",
                   "channel_snrs", "chi2", "red_chi2", "snr", "nfev", "status",
                   "init_used", "fun", "cov_nosc", "grad", "hess"]:
             setattr(res, k, _ptr(out[k]))
+        res.errs_out = _ptr(out["errs"])
         self._chk(self.lib.ppf_fit_portrait_batch(self.ctx, ctypes.byref(desc),
                                                   ctypes.byref(res)))
         out["_keep"] = keep  # inputs must outlive the stream-ordered call

@@ -92,13 +92,20 @@ def _units(opened, model_data):
     nch = len(mf)
     mok = model_data.ok_ichans[0]
     model_full = len(mok) == nch
+    mfq = np.asarray(model_data.freqs)
+    mbytes = mfq.tobytes()
     for name, a in opened:
         m = a.meta
-        try:
-            fd = m.freqs - model_data.freqs
-            same = fd.min() == fd.max() == 0.0
-        except ValueError:
-            same = False
+        f = m.freqs
+        if isinstance(f, np.ndarray) and f.shape == mfq.shape and f.dtype == mfq.dtype and \
+                f.tobytes() == mbytes and not np.isnan(f).any():
+            same = True  # identical values: fd is 0 everywhere
+        else:
+            try:
+                fd = f - model_data.freqs
+                same = fd.min() == fd.max() == 0.0
+            except ValueError:
+                same = False
         for isub in m.ok_isubs:
             if same:
                 oi = m.ok_ichans[isub]
@@ -135,30 +142,32 @@ def _is_full(ichans, mich, full_rows):
         np.array_equal(ichans, mich)
 
 
-def _elem_stride(rows):
-    return (rows[1].data_ptr() - rows[0].data_ptr()) // rows[0].element_size() \
-        if len(rows) > 1 else rows[0][0].numel()
+def _strided_rows(rows):
+    """rows: (t, j) pairs naming t[j] of float64 tensors [k, npol=1, nchan,
+    nbin].  When every t[j] is a contiguous [1, nchan, nbin] row and they are
+    equally spaced in one storage, returns one [n, nchan, nbin] view of them
+    all (no copy); else None."""
+    t0, j0 = rows[0]
+    if t0.dim() != 4 or t0.shape[1] != 1 or t0.dtype != torch.float64:
+        return None
+    shape = t0.shape[1:]
+    nchan, nbin = shape[1], shape[2]
 
+    def ptr(t, j):
+        return t.data_ptr() + j * t.stride(0) * 8
 
-def _uniform_rows(rows):
-    """rows [npol=1, nchan, nbin] tensors that are equally spaced views of one
-    storage (each contiguous, same device/dtype, positive stride)."""
-    r0 = rows[0]
-    if r0.dim() != 3 or r0.shape[0] != 1 or not r0.is_contiguous() or \
-            r0.dtype != torch.float64:
-        return False
-    if len(rows) == 1:
-        return True
-    st = rows[1].data_ptr() - r0.data_ptr()
-    if st < r0.numel() * r0.element_size() or st % r0.element_size():
-        return False
-    base = r0.untyped_storage().data_ptr()
-    p0 = r0.data_ptr()
-    for j, r in enumerate(rows):
-        if r.data_ptr() != p0 + j * st or not r.is_contiguous() or r.shape != r0.shape or \
-                r.device != r0.device or r.untyped_storage().data_ptr() != base:
-            return False
-    return True
+    p0 = ptr(t0, j0)
+    st = (ptr(*rows[1]) - p0) if len(rows) > 1 else nchan * nbin * 8
+    if st < nchan * nbin * 8 or st % 8:
+        return None
+    base = t0.untyped_storage().data_ptr()
+    for k, (t, j) in enumerate(rows):
+        if ptr(t, j) != p0 + k * st or t.shape[1:] != shape or \
+                (nbin > 1 and t.stride(3) != 1) or (nchan > 1 and t.stride(2) != nbin) or \
+                t.untyped_storage().data_ptr() != base:
+            return None
+    off = t0.storage_offset() + j0 * t0.stride(0)
+    return t0.as_strided((len(rows), nchan, nbin), (st // 8, nbin, 1), off)
 
 
 class _UnitStack:
@@ -194,12 +203,16 @@ class _UnitStack:
         partial_units = [i for i, u in enumerate(units) if not _is_full(u[2], u[3], full_rows)]
         if partial_units or npol != 1:
             self.pols = [torch.empty((n, nchan, nbin), **f64) for _ in range(npol)]
-        full_i, full_f, full_w, full_s, full_e = [], [], [], [], []
+        full_f, full_w, full_s, full_e = [], [], [], []
         for name, idx in by_arch.items():
             a = arch[name]
             m = a.meta
-            isubs = np.array([units[i][1] for i in idx])
-            lo, hi = int(isubs.min()), int(isubs.max()) + 1
+            if len(idx) == 1:
+                lo = units[idx[0]][1]
+                hi = lo + 1
+            else:
+                isubs = [units[i][1] for i in idx]
+                lo, hi = min(isubs), max(isubs) + 1
             sub = a.read(lo, hi)  # this rank's subint range only
             if not isinstance(sub, torch.Tensor):
                 sub = torch.as_tensor(np.ascontiguousarray(sub), device=dev)
@@ -209,37 +222,35 @@ class _UnitStack:
                 snrs[lo:hi] = a.snrs(sub)
             ns = m.get("noise_stds")
             ns = None if ns is None else np.asarray(ns)
+            Ps, DM, mfreqs, mwts = m.Ps, m.DM, m.freqs, m.weights
             # device rows, and the host arrays of this archive's units (full
-            # units as row views, stacked once for all archives below)
+            # units as (tensor, row) pairs, stacked once for all archives below)
             for i in idx:
                 _, isub, ichans, mich = units[i]
-                P[i] = m.Ps[isub]
-                DMg[i] = m.DM
+                P[i] = Ps[isub]
+                DMg[i] = DM
                 if _is_full(ichans, mich, full_rows):
                     frow.append(i)
-                    fsrc.append(sub[isub - lo])
-                    full_i.append(i)
-                    full_f.append(m.freqs[isub])
-                    full_w.append(m.weights[isub])
+                    fsrc.append((sub, isub - lo))
+                    full_f.append(mfreqs[isub])
+                    full_w.append(mwts[isub])
                     full_s.append(snrs[isub, 0])
-                    if ns is not None:
-                        full_e.append(ns[isub, 0])
-                    else:
-                        full_e.append(None)
+                    full_e.append(None if ns is None else ns[isub, 0])
                     continue
                 ic = torch.as_tensor(ichans, device=dev, dtype=torch.long)
                 mc = torch.as_tensor(mich, device=dev, dtype=torch.long)
                 for ipol in range(npol):
                     self.pols[ipol][i].zero_()
                     self.pols[ipol][i].index_copy_(0, mc, sub[isub - lo, ipol].index_select(0, ic))
-                freqs[i, mich] = m.freqs[isub, ichans]
+                freqs[i, mich] = mfreqs[isub, ichans]
                 if ns is not None:
                     errs[i, mich] = ns[isub, 0, ichans]
                 else:
                     need_noise[i] = True
                 mask[i, mich] = 1
-                wts[i, mich] = m.weights[isub, ichans]
-                nu_fit[i] = guess_fit_freq(m.freqs[isub, ichans], snrs[isub, 0, ichans])
+                wts[i, mich] = mwts[isub, ichans]
+                nu_fit[i] = guess_fit_freq(mfreqs[isub, ichans], snrs[isub, 0, ichans])
+        full_i = frow
         if full_i:
             rows = np.array(full_i)
             fr = np.stack(full_f)
@@ -251,21 +262,23 @@ class _UnitStack:
                 errs[rows[have]] = np.stack([e for e in full_e if e is not None])
             need_noise[rows[~have]] = True
             nu_fit[rows] = _guess_fit_freq_rows(fr, np.stack(full_s))
-        if frow and npol == 1 and frow == list(range(n)) and _uniform_rows(fsrc):
+        view = _strided_rows(fsrc) if (frow and npol == 1 and frow == list(range(n))) else None
+        if view is not None:
             # every unit a full row of one strided tensor (rows of the caller's
-            # own stack): use it in place, no copy
-            self.pols = [fsrc[0].as_strided((n, nchan, nbin), (_elem_stride(fsrc), nbin, 1))]
+            # own stack), in unit order: use it in place, no copy
+            self.pols = [view]
         elif frow:  # one gather per polarisation for every full unit
             if self.pols[0] is None:
                 self.pols = [torch.empty((n, nchan, nbin), **f64) for _ in range(npol)]
             dst = torch.as_tensor(np.array(frow), device=dev, dtype=torch.long)
-            src = torch.stack(fsrc)  # [nfull, npol, nchan, nbin]
+            src = torch.stack([t[j] for t, j in fsrc])  # [nfull, npol, nchan, nbin]
             for ipol in range(npol):
                 self.pols[ipol].index_copy_(0, dst, src[:, ipol])
             del src
-        if need_noise.any():  # load_data's noise_stds (pplib.py:2744-2748), on the device
-            noise = eng.noise_rows(self.pols[0].reshape(-1, nbin)).reshape(n, nchan).cpu().numpy()
-            errs = np.where(need_noise[:, None] & (mask > 0), noise, errs)
+        # load_data's noise_stds (pplib.py:2744-2748) where the archive has
+        # none: NaN here, so the fit's data pass estimates them from the same
+        # rows it transforms (get_noise_PS) and returns them (fit "errs")
+        errs = np.where(need_noise[:, None] & (mask > 0), np.nan, errs)
         self.freqs, self.errs, self.mask, self.wts = freqs, errs, mask, wts
         self.P, self.DMg, self.nu_fit = P, DMg, nu_fit
 
@@ -283,7 +296,6 @@ class _UnitStack:
             init = np.stack([np.zeros(n), self.DMg, np.zeros(n), np.zeros(n), np.zeros(n)], 1)
             self._dv = dict(P=torch.as_tensor(self.P, **f64),
                             f2=torch.as_tensor(self.freqs ** -2.0, **f64),
-                            e2=torch.as_tensor(self.errs ** 2, **f64),
                             on=torch.as_tensor(self.mask > 0, device=dev),
                             init=torch.as_tensor(init, **f64),
                             freqs=torch.as_tensor(self.freqs, **f64),
@@ -301,14 +313,16 @@ class _UnitStack:
                                   guess_nu=dv["nu"], to_host=False)
         if mark is not None:
             t0 = mark("fit", t0)
-        out = {k: torch.as_tensor(out[k], device=dev) for k in ("params", "nu_out", "scales")}
+        out = {k: torch.as_tensor(out[k], device=dev) for k in ("params", "nu_out", "scales",
+                                                                "errs")}
         phase = out["params"][:, 0]
         DM = out["params"][:, 1]
         nu_ref = out["nu_out"][:, 0]
         # rotate_data(port, phase, DM, P, freqs, nu_ref) per channel (pplib.py:2406-2415)
         ph = phase[:, None] + (Dconst * DM / dv["P"])[:, None] * (dv["f2"] - nu_ref[:, None] ** -2.0)
-        w = torch.where(dv["on"], out["scales"] / dv["e2"], torch.zeros((), dtype=torch.float64,
-                                                                       device=dev))
+        e2 = torch.as_tensor(out["errs"], device=dev) ** 2  # the sigma each channel was fitted with
+        w = torch.where(dv["on"], out["scales"] / e2, torch.zeros((), dtype=torch.float64,
+                                                                 device=dev))
         for ipol, pol in enumerate(self.pols):
             eng.rotate_accumulate(pol, ph, w, accum[ipol])
         tw += w.sum(dim=0).to(tw.device)

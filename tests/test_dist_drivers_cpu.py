@@ -49,7 +49,16 @@ def fake_fit(data, model, init, P, freqs, nu_fits=None, nu_outs=None, errs=None,
         kw["log_calls"].append(nsub)
     cov = np.zeros((nsub, 5, 5))
     cov[:, 0, 0], cov[:, 1, 1], cov[:, 0, 1] = 1e-8, 4e-8, 1e-9
-    return dict(params=params, param_errs=errs5, nu_out=nu.copy(), cov=cov, scales=sc,
+    # the sigma each channel is fitted with: errs, get_noise_PS where NaN, 0 masked
+    e = np.full((nsub, nchan), np.nan) if errs is None else \
+        np.array(np.broadcast_to(np.asarray(errs, float), (nsub, nchan)))
+    if np.isnan(e).any():
+        from oracle import ppfit_oracle as O
+        ps = O.get_noise_PS(data.reshape(-1, nbin), chans=True).reshape(nsub, nchan)
+        e = np.where(np.isnan(e), ps, e)
+    if chan_mask is not None:
+        e = np.where(np.asarray(chan_mask) > 0, e, 0.0)
+    return dict(params=params, param_errs=errs5, nu_out=nu.copy(), cov=cov, scales=sc, errs=e,
                 scale_errs=0.1 * sc, channel_snrs=10 * sc, chi2=b, red_chi2=b / (nchan * nbin),
                 snr=np.sqrt(b), nfev=np.full(nsub, 5, np.int32), status=np.full(nsub, 2, np.int32),
                 duration=np.zeros(nsub))

@@ -242,18 +242,20 @@ TNC_R2 = [6, 7, 8, 9]
 def test_fit_full_r2_tnc(eng, golden, ic):
     """Device TNC against the reference's TNC.  TNC stops at the rounding
     floor: a converged fit ends FCONVERGED (1) or LSFAIL (4) depending on the
-    last bits of f (scipy itself flips between them when the start moves by
-    one ulp, tests/test_tnc_model.py), so converged statuses only have to stay
-    in the set the reference accepts (pptoaslib.py:1022); a fit that ran into
-    maxfun (3) must do so too, after the same 100 evaluations."""
-    from tests._compare import CONVERGED, phase_gap
+    last bits of f (the reference itself flips between them when its start
+    moves by one ulp: tnc_floor.npz), so the status must be the reference's
+    or one of that floor set; a fit that ran into maxfun (3) must do so too,
+    after the same 100 evaluations."""
+    from tests._compare import phase_gap
     f = golden("fit_full_r2.npz")
     k = "f%d_" % ic
     r = fit_r2(eng, f, ic)
     ref_rc = int(f[k + "return_code"])
     rc = int(r["status"][0])
-    if rc != ref_rc:
-        assert {rc, ref_rc} <= CONVERGED, (rc, ref_rc)
+    # the reference's status, or one the reference itself returns when its
+    # start moves by one ulp (tnc_floor.npz; f9: 1 or 4)
+    floor = set(int(v) for v in golden("tnc_floor.npz")[k + "rcs"])
+    assert rc in floor | {ref_rc}, (rc, ref_rc, sorted(floor))
     if ref_rc == 3:
         assert rc == 3 and int(r["nfev"][0]) == int(f[k + "nfeval"])
     # A converged fit ends within north_star's 1e-3 sigma of the reference's
@@ -283,14 +285,13 @@ def test_fit_full_r2_tnc(eng, golden, ic):
 def test_legacy_fit_portrait_tnc(eng, golden, ic):
     """pplib.fit_portrait (legacy TNC, 2 parameters) against the reference."""
     from pulseportraiture_amd import pplib
-    from tests._compare import CONVERGED
     g = golden("legacy_fit_portrait.npz")
     k = "l%d_" % ic
     r = pplib.fit_portrait(g[k + "data"], g[k + "model"], g[k + "init"], P0, g[k + "freqs"],
                            float(g[k + "nu_fit"]), None, g[k + "errs"])
     ref_rc = int(g[k + "return_code"])
-    if r.return_code != ref_rc:
-        assert {r.return_code, ref_rc} <= CONVERGED, (r.return_code, ref_rc)
+    floor = set(int(v) for v in golden("tnc_floor.npz")[k + "rcs"])
+    assert r.return_code in floor | {ref_rc}, (r.return_code, ref_rc, sorted(floor))
     # phases compared at the reference's zero-covariance frequency (each fit
     # reports its own); north_star's 1e-3 sigma
     from tests._compare import phi_at

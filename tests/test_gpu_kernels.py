@@ -145,11 +145,13 @@ def test_synth_matches_numpy(eng):
     np.testing.assert_allclose(got, ref, atol=1e-11)
 
 
-@pytest.mark.parametrize("nsub,nchan,nbin", [(5, 6, 128), (37, 10, 2048), (3, 3, 2048)])
+@pytest.mark.parametrize("nsub,nchan,nbin", [(5, 6, 128), (37, 10, 2048), (3, 3, 2048),
+                                              (45, 300, 2048)])
 def test_rotate_accumulate(eng, nsub, nchan, nbin):
     """Fourier-domain rotate-and-sum of ppalign (ppalign.py:202-208); nbin 2048
     takes the one-wave-per-row register-FFT kernel (k_rot_accum_w), including
-    a channel count that leaves a workgroup's last waves without a row."""
+    slices shorter than a group of four rows (3 x 3, 37 x 10) and slices of
+    seven rows: a full group and a ragged one (45 x 300, 7 slices)."""
     import torch
     rng = np.random.default_rng(9)
     data = rng.normal(0, 1, (nsub, nchan, nbin))

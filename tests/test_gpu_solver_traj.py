@@ -129,11 +129,19 @@ def test_solver_follows_reference_trajectory(eng, tag):
 @pytest.mark.parametrize("tag", ["f6", "f8", "f9", "f10"] + LEGACY_CASES)
 def test_converged_end_point_within_1e3_sigma(eng, tag):
     """Converged TNC / Newton-CG fits end within 1e-3 sigma of the reference
-    (phase compared at the reference's output frequency)."""
-    from tests._compare import CONVERGED, phase_gap
+    (phase compared at the reference's output frequency), with the
+    reference's status or one of its one-ulp floor (f10, Newton-CG: 2)."""
+    from tests._compare import phase_gap
     c = _case(tag)
     res, _ = _device(eng, c)
-    assert {int(res["status"]), c["rc"]} <= CONVERGED
+    # the status is the reference's, or one the reference itself returns when
+    # its start moves by one ulp (tnc_floor.npz: f9 ends with 1 or 4 -- the
+    # final line search fails or f has converged, decided by the last bits)
+    tf = _load("tnc_floor.npz")
+    floor = set(int(v) for v in tf[tag + "_rcs"]) if tag + "_rcs" in tf.files else set()
+    print("%s: status %d (reference %d, its one-ulp floor %s)" % (
+        tag, int(res["status"]), c["rc"], sorted(floor)))
+    assert int(res["status"]) in floor | {c["rc"]}
     p = res["params"]
     if tag.startswith("l"):
         from pulseportraiture_amd import pplib
