@@ -358,6 +358,18 @@ __global__ __launch_bounds__(kBlock, 3) void k_fit_taylor(FitArgs a) {
   const int c = blockIdx.x, s = a.sub0 + c, tid = threadIdx.x;
   const int lane = tid & 63;
   if (!fused_taylor(a, s)) return;
+  // diagnostic phase clock (ppf_phase_profile): thread 0 only
+  const bool prof = a.ptime != nullptr;
+  unsigned long long t0 = prof ? wall_clock64() : 0ull;
+  unsigned long long pt[5] = {0, 0, 0, 0, 0};
+  unsigned long long nrc = 0;
+  auto mark = [&](int i) {
+    if (prof && tid == 0) {
+      const unsigned long long t1 = wall_clock64();
+      pt[i] += t1 - t0;
+      t0 = t1;
+    }
+  };
   if constexpr (MOM) {
     const SolveState& st0 = a.st[c];
     const int w = tid >> 6;
@@ -373,18 +385,7 @@ __global__ __launch_bounds__(kBlock, 3) void k_fit_taylor(FitArgs a) {
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   }
-  // diagnostic phase clock (ppf_phase_profile): thread 0 only
-  const bool prof = a.ptime != nullptr;
-  unsigned long long t0 = prof ? wall_clock64() : 0ull;
-  unsigned long long pt[5] = {0, 0, 0, 0, 0};
-  unsigned long long nrc = 0;
-  auto mark = [&](int i) {
-    if (prof && tid == 0) {
-      const unsigned long long t1 = wall_clock64();
-      pt[i] += t1 - t0;
-      t0 = t1;
-    }
-  };
+  mark(0);  // slot 0: the fused first moment pass
   unsigned char* dmeta = dyn;
   SolveState& st = a.st[c];
   // T slot 0 (k_moments) read once into LDS: every sweep about centre 0 then

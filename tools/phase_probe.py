@@ -13,6 +13,8 @@ from pulseportraiture_amd.engine import Engine  # noqa: E402
 nsub = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
 nchan, nbin = 64, 2048
 eng = Engine(0)
+if "sep" in sys.argv[2:]:  # the first moment pass in its own launch (k_moments)
+    eng.set_option("fuse_moments", 0)
 dev = eng.device
 w = synth.make_workload(nsub, nchan, nbin, seed=20240917)
 data = eng.synth(w.template, w.phase, w.sigma, w.seed, sub0=w.sub0)
@@ -63,7 +65,7 @@ pt = eng.phase_profile(False)
 nwg = max(pt[9], 1)
 print("phase clocks per workgroup (us):",
       {n: round(pt[i] / nwg / 100.0, 2) for i, n in
-       enumerate(["guess", "meta+moments0", "centre", "sweep", "trstep"])},
+       enumerate(["moment pass (fused)", "meta+T0", "centre", "sweep", "trstep"])},
       "recentres/subint", pt[8] / nwg, "workgroups", pt[9],
       "guess brute/NM us", round(pt[10] / nwg / 100.0, 2), round(pt[11] / nwg / 100.0, 2),
       "NM calls", pt[12] / nwg)
