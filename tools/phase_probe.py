@@ -69,3 +69,14 @@ print("phase clocks per workgroup (us):",
       "recentres/subint", pt[8] / nwg, "workgroups", pt[9],
       "guess brute/NM us", round(pt[10] / nwg / 100.0, 2), round(pt[11] / nwg / 100.0, 2),
       "NM calls", pt[12] / nwg)
+
+# the fused kernel with one objective sweep and no solver steps (eval_only):
+# the moment pass + meta + one sweep, i.e. the streaming part alone
+eng.set_timing(True)
+eng.reset_kernel_times()
+for _ in range(3):
+    eng.fit_batch(data, model, freqs, P, init0, flags, nu_fit=nu, guess=True, guess_Ns=100,
+                  eval_only=True)
+torch.cuda.synchronize()
+print("eval_only      ", {k: round(eng.kernel_time(k)[0] / 3, 3) for k in names})
+eng.set_timing(False)
