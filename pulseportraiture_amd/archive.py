@@ -356,6 +356,15 @@ class Archive:
         from .engine import get_engine
         return get_engine().profile_snr(sub).cpu().numpy()
 
+    def registered_rows(self):
+        """The registered subints tensor itself (every subint, nothing to
+        process), or None: a reader of a few rows of it can index it directly
+        instead of slicing read(lo, hi)."""
+        if self._reg is None or self.tscrunch or self.rot_sign or self.rm_base:
+            return None
+        sub = self._reg.base.subints
+        return sub if _is_tensor(sub) else None
+
     def read(self, lo=0, hi=None):
         if self.tscrunch:  # the one averaged subint needs every raw subint
             from .engine import get_engine

@@ -152,21 +152,37 @@ def _strided_rows(rows):
         return None
     shape = t0.shape[1:]
     nchan, nbin = shape[1], shape[2]
-
-    def ptr(t, j):
-        return t.data_ptr() + j * t.stride(0) * 8
-
-    p0 = ptr(t0, j0)
-    st = (ptr(*rows[1]) - p0) if len(rows) > 1 else nchan * nbin * 8
+    # one storage: every row a view of t0's base (a cheap identity test), or
+    # failing that the storages' own addresses
+    base0 = t0._base
+    sbase = None if base0 is not None else t0.untyped_storage().data_ptr()
+    st0 = t0.stride()
+    if (nbin > 1 and st0[3] != 1) or (nchan > 1 and st0[2] != nbin):
+        return None
+    p0 = t0.data_ptr() + j0 * st0[0] * 8
+    if len(rows) > 1:
+        t1, j1 = rows[1]
+        st = t1.data_ptr() + j1 * t1.stride(0) * 8 - p0
+    else:
+        st = nchan * nbin * 8
     if st < nchan * nbin * 8 or st % 8:
         return None
-    base = t0.untyped_storage().data_ptr()
-    for k, (t, j) in enumerate(rows):
-        if ptr(t, j) != p0 + k * st or t.shape[1:] != shape or \
-                (nbin > 1 and t.stride(3) != 1) or (nchan > 1 and t.stride(2) != nbin) or \
-                t.untyped_storage().data_ptr() != base:
+    p = p0
+    for t, j in rows:
+        if t is not t0:
+            if (t._base is not base0 if base0 is not None else
+                    t.untyped_storage().data_ptr() != sbase) or t.shape[1:] != shape:
+                return None
+            stt = t.stride()
+            if stt[2:] != st0[2:]:
+                return None
+            q = t.data_ptr() + j * stt[0] * 8
+        else:
+            q = t.data_ptr() + j * st0[0] * 8
+        if q != p:
             return None
-    off = t0.storage_offset() + j0 * t0.stride(0)
+        p += st
+    off = t0.storage_offset() + j0 * st0[0]
     return t0.as_strided((len(rows), nchan, nbin), (st // 8, nbin, 1), off)
 
 
@@ -213,7 +229,11 @@ class _UnitStack:
             else:
                 isubs = [units[i][1] for i in idx]
                 lo, hi = min(isubs), max(isubs) + 1
-            sub = a.read(lo, hi)  # this rank's subint range only
+            reg = a.registered_rows()
+            if reg is not None:  # the caller's own registered tensor, no slicing
+                sub, lo = reg, 0
+            else:
+                sub = a.read(lo, hi)  # this rank's subint range only
             if not isinstance(sub, torch.Tensor):
                 sub = torch.as_tensor(np.ascontiguousarray(sub), device=dev)
             snrs = m.SNRs
