@@ -52,7 +52,9 @@ def _ptr(t):
 
 def _nan_none(x):
     """Array-like that may contain None (reference 'use the default') -> float64 with NaN."""
-    a = np.asarray(x, dtype=object)
+    a = np.asarray(x)
+    if a.dtype != object:  # no None in it
+        return a.astype(np.float64)
     return np.array([np.nan if v is None else float(v) for v in a.ravel()],
                     dtype=np.float64).reshape(a.shape)
 

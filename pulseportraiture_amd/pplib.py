@@ -524,12 +524,14 @@ def _flag_text(flag, value):
     return _flag_fmt(flag, type(value)) % value
 
 
-_LINE_FMTS = {}  # (flag, type) signature of a TOA's flags -> their joined format
+_LINE_FMTS = {}  # (flag names, value types) of a TOA's flags -> their joined format
+_NoneType = type(None)
 
 
 def toa_line(toa, inf_is_zero=True):
     """One loosely-IPTA .tim line, pplib.py:3471-3503.  The flags of every TOA
-    with the same (flag, value type) signature share one format string."""
+    with the same (flag, value type) signature share one format string; a
+    None value is left out, as write_TOAs skips it."""
     freq = 0.0 if (toa.frequency == np.inf and inf_is_zero) else toa.frequency
     m = toa.MJD
     s = "%s %.8f %d" % (toa.archive, freq, m.intday()) + \
@@ -538,14 +540,18 @@ def toa_line(toa, inf_is_zero=True):
         s += " -pp_dm %.7f" % toa.DM
     if toa.DM_error is not None:
         s += " -pp_dme %.7f" % toa.DM_error
-    items = [(k, v) for k, v in toa.flags.items() if v is not None]
-    sig = tuple([(k, type(v)) for k, v in items])
-    fmt = _LINE_FMTS.get(sig)
+    fl = toa.flags
+    vals = tuple(fl.values())
+    types = tuple(map(type, vals))
+    key = (tuple(fl), types)
+    fmt = _LINE_FMTS.get(key)
     if fmt is None:
-        fmt = "".join([_flag_fmt(k, t) for k, t in sig])
+        fmt = "".join([_flag_fmt(k, t) for k, t in zip(key[0], types) if t is not _NoneType])
         if len(_LINE_FMTS) < 4096:
-            _LINE_FMTS[sig] = fmt
-    return s + fmt % tuple([v for _, v in items])
+            _LINE_FMTS[key] = fmt
+    if _NoneType in types:
+        vals = tuple([v for v in vals if v is not None])
+    return s + fmt % vals
 
 
 def write_TOAs(TOAs, inf_is_zero=True, SNR_cutoff=0.0, outfile=None, append=True):
