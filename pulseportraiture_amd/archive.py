@@ -376,6 +376,48 @@ class Archive:
         return self._process(self._read_src(lo, hi), lo, hi)
 
 
+class _RegisteredView:
+    """A registered archive opened for reading only, when the request has
+    nothing to process (Archive would copy its metadata unchanged): the
+    metadata IS the registered bunch (callers must not modify it), reads are
+    views of its subints.  Used by drivers that open many archives at once
+    (ppalign) to skip the per-archive copies."""
+    owns_reads = False
+    eager_noise = False
+    tscrunch = False
+    rot_sign = 0.0
+    rm_base = False
+    snrs = staticmethod(Archive.snrs)
+
+    def __init__(self, base):
+        self.meta = self.raw = base
+
+    @property
+    def nsub(self):
+        return self.meta.nsub
+
+    def registered_rows(self):
+        sub = self.meta.subints
+        return sub if _is_tensor(sub) else None
+
+    def read(self, lo=0, hi=None):
+        return self.meta.subints[lo:(self.meta.nsub if hi is None else hi)]
+
+
+def registered_view(filename, dedisperse=False, dededisperse=False, tscrunch=False,
+                    rm_baseline=True):
+    """A read-only _RegisteredView of a registered archive when opening it
+    with these options would process nothing, else None (use open_archive)."""
+    b = _registry.get(filename) if isinstance(filename, str) else None
+    if b is None:
+        return None
+    dmc = int(b.get("dmc", 0))
+    if (dedisperse and not dmc) or (dededisperse and dmc) or (tscrunch and b.nsub > 1) or \
+            (rm_baseline and not b.get("baseline_removed", True)):
+        return None
+    return _RegisteredView(b)
+
+
 def open_archive(filename, dedisperse=False, dededisperse=False, tscrunch=False, pscrunch=False,
                  rm_baseline=True, quiet=True):
     """Metadata now, subints on demand (see Archive)."""

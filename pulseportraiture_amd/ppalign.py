@@ -54,7 +54,10 @@ def _open_all(datafiles, model_data, SNR_cutoff, quiet, skip_these, tscrunch, ps
     out = []
     for name in datafiles:
         try:  # ppalign.py:123-127 (rm_baseline False: F0_fact = 0, pptoas.py:26-29)
-            a = _arch.open_archive(name, dedisperse=False, tscrunch=tscrunch, pscrunch=pscrunch,
+            # a registered archive with nothing to process is read in place
+            a = _arch.registered_view(name, dedisperse=False, tscrunch=tscrunch,
+                                      rm_baseline=rm_baseline) or \
+                _arch.open_archive(name, dedisperse=False, tscrunch=tscrunch, pscrunch=pscrunch,
                                    rm_baseline=rm_baseline, quiet=True)
         except RuntimeError:
             if not quiet:
