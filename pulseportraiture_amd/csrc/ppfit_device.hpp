@@ -6,9 +6,12 @@
 #pragma once
 
 #ifndef PPF_NT
-// streaming (non-temporal) hints on the data pass's read-once portrait rows
-// and write-once cross-spectrum rows: 5.57 -> 5.04 ms at config 2 (r02; the
-// moment pass's X loads were slower with the hint and stay plain)
+// streaming (non-temporal) hint on the data pass's read-once portrait rows:
+// with the write-once X stores, 5.57 -> 5.04 ms at config 2 (r02; the moment
+// pass's X loads were slower with the hint and stay plain).  r04: the stores
+// are plain again (PPF_NT_ST below); on the loads the hint is worth 0.15-0.27
+// ms of the config-5 data pass (256-channel template blocks stay in L2) and
+// is within box-to-box noise at config 2
 #define PPF_NT 1
 #endif
 #ifndef PPF_EARLY_ROW
