@@ -325,8 +325,17 @@ __host__ __device__ inline int pfa_scratch_slots(int Ns, int NH) {
 // within rounding (1e-12 relative) of it -- then the caller re-takes the grid
 // by direct sums, as for the folded grid.
 __device__ inline bool pfa_pass(const double2* rm, int NH, double ie2, int Ns, double lo,
-                                double hi, GuessShared& gs, double2* scr, int A, int B) {
+                                double hi, GuessShared& gs, double2* scr, int A, int B,
+                                unsigned long long* clk = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  unsigned long long tc = clk ? wall_clock64() : 0ull;
+  auto tick = [&](int slot) {  // diagnostic: [4 + slot] phase clocks of this pass
+    if (clk && tid == 0) {
+      const unsigned long long t = wall_clock64();
+      atomicAdd(&clk[4 + slot], t - tc);
+      tc = t;
+    }
+  };
   const int L = Ns - 1;
   double2* Y = scr;
   double2* wB = scr + L;
@@ -342,28 +351,83 @@ __device__ inline bool pfa_pass(const double2* rm, int NH, double ie2, int Ns, d
     wA[m] = cmk(cs, sn);
   }
   __syncthreads();
-  // stage 1: Y[n1][k2] = sum_{n2 < B} b_{(B n1 + A n2) mod L} W_B^{n2 k2}
+  tick(0);
+  // stage 1: Y[n1][k2] = sum_{n2 < B} b_{(B n1 + A n2) mod L} W_B^{n2 k2}, the
+  // terms in four independent running sums (n2 mod 4) so that four LDS reads
+  // are in flight instead of one dependent chain; with NH <= L every folded
+  // b_j is one signed harmonic or 0.  (Only the argmin is taken from these
+  // values, and any grid point within 1e-12 of it sends the caller to the
+  // direct sums: the order of the additions cannot change the result.)
+  const bool one = NH <= L;
+  // branch-free when every fold has at most one term (an unconditional LDS
+  // read and a select): the loop below then stays one basic block, so its
+  // four terms' reads overlap
+  auto bj = [&](int j) {
+    if (one) {
+      const double2 r = rm[min(j, NH - 1)];
+      const double sg = j < NH ? ((j & 1) ? -1.0 : 1.0) : 0.0;
+      return cmk(sg * r.x, sg * r.y);
+    }
+    double2 b = cmk(0.0, 0.0);
+    for (int k = j; k < NH; k += L) b = (k & 1) ? csub(b, rm[k]) : cadd(b, rm[k]);
+    return b;
+  };
+  // The twiddles W_B^{n2 k2} of a lane's output run along its own chain
+  // (times W_B^{4 k2} per block of four terms) instead of a table read per
+  // term: the B-entry table is read by every lane at a different index, and
+  // those bank-conflicted reads made this stage LDS-bound.  Each chain is
+  // re-seeded exactly from the table every 32 terms.
+  auto stage1 = [&](auto onec) {
+  constexpr bool ONE = decltype(onec)::value;
+  auto bj1 = [&](int j) {
+    if constexpr (ONE) {
+      const double2 r = rm[min(j, NH - 1)];
+      const double sg = j < NH ? ((j & 1) ? -1.0 : 1.0) : 0.0;
+      return cmk(sg * r.x, sg * r.y);
+    } else {
+      return bj(j);
+    }
+  };
   for (int q = tid; q < L; q += kBlock) {
     const int n1 = q / B, k2 = q - n1 * B;
-    int j = (B * n1) % L, m = 0;
-    double2 acc = cmk(0.0, 0.0);
-    for (int n2 = 0; n2 < B; ++n2) {
-      double2 b = cmk(0.0, 0.0);
-      for (int k = j; k < NH; k += L) b = (k & 1) ? csub(b, rm[k]) : cadd(b, rm[k]);
-      acc = cadd(acc, cmul(b, wB[m]));
-      j += A;
-      if (j >= L) j -= L;
-      m += k2;
-      if (m >= B) m -= B;
+    int j = (B * n1) % L;
+    const double2 st4 = wB[(4 * k2) % B];
+    double2 acc[4] = {cmk(0.0, 0.0), cmk(0.0, 0.0), cmk(0.0, 0.0), cmk(0.0, 0.0)};
+    double2 tw[4];
+    int n2 = 0;
+    for (; n2 + 4 <= B; n2 += 4) {
+      if ((n2 & 31) == 0) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) tw[u] = wB[((n2 + u) * k2) % B];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        acc[u] = cadd(acc[u], cmul(bj1(j), tw[u]));
+        tw[u] = cmul(tw[u], st4);
+        j += A;
+        if (j >= L) j -= L;
+      }
     }
-    Y[q] = acc;
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {  // the B mod 4 last terms
+      if (n2 + u < B) {
+        acc[u] = cadd(acc[u], cmul(bj1(j), wB[((n2 + u) * k2) % B]));
+        j += A;
+        if (j >= L) j -= L;
+      }
+    }
+    Y[q] = cadd(cadd(acc[0], acc[1]), cadd(acc[2], acc[3]));
   }
+  };
+  if (one) stage1(std::true_type{});
+  else stage1(std::false_type{});
   __syncthreads();
-  // stage 2 and the per-thread grid values
+  tick(1);
+  // stage 2 and the per-thread grid values (int arithmetic: B Ai, A Bi <= L)
   int Ai = 1, Bi = 1;  // B^-1 mod A, A^-1 mod B
-  while ((long long)B * Ai % A != 1) ++Ai;
-  while ((long long)A * Bi % B != 1) ++Bi;
-  const long long cB = (long long)B * Ai, cA = (long long)A * Bi;
+  while (B * Ai % A != 1) ++Ai;
+  while (A * Bi % B != 1) ++Bi;
+  const int cB = B * Ai % L, cA = A * Bi % L;
   double vals[kPfaPer];
   int gi[kPfaPer];
   double bv = NAN;
@@ -375,16 +439,30 @@ __device__ inline bool pfa_pass(const double2* rm, int NH, double ie2, int Ns, d
     gi[r] = 0x7fffffff;
     if (q < L) {
       const int k1 = q / B, k2 = q - k1 * B;
-      double re = 0.0;
-      int m = 0;
-      for (int n1 = 0; n1 < A; ++n1) {
-        const double2 y = Y[n1 * B + k2], t = wA[m];
-        re = fma(y.x, t.x, re);
-        re = fma(-y.y, t.y, re);
-        m += k1;
-        if (m >= A) m -= A;
+      double rs[4] = {0.0, 0.0, 0.0, 0.0};
+      int m = 0, n1 = 0;
+      for (; n1 + 4 <= A; n1 += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const double2 y = Y[(n1 + u) * B + k2], t = wA[m];
+          rs[u] = fma(y.x, t.x, rs[u]);
+          rs[u] = fma(-y.y, t.y, rs[u]);
+          m += k1;
+          if (m >= A) m -= A;
+        }
       }
-      const int g = (int)((cB * k1 + cA * k2) % L);
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {  // the A mod 4 last terms
+        if (n1 + u < A) {
+          const double2 y = Y[(n1 + u) * B + k2], t = wA[m];
+          rs[u] = fma(y.x, t.x, rs[u]);
+          rs[u] = fma(-y.y, t.y, rs[u]);
+          m += k1;
+          if (m >= A) m -= A;
+        }
+      }
+      const double re = (rs[0] + rs[1]) + (rs[2] + rs[3]);
+      const int g = (cB * k1 + cA * k2) % L;
       const double f = -re * ie2;
       vals[r] = f;
       gi[r] = g;
@@ -397,6 +475,7 @@ __device__ inline bool pfa_pass(const double2* rm, int NH, double ie2, int Ns, d
     const int oi = __shfl_xor(bi, o);
     if (argmin_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
   }
+  tick(2);
   if (lane == 0) { gs.bestv[w] = bv; gs.besti[w] = bi; }
   __syncthreads();
   if (tid == 0) {
@@ -424,7 +503,8 @@ __device__ inline void guess_search(const double2* rm, int NH, double ie2, int N
                                     unsigned long long* clk = nullptr,
                                     double2* pfa_scr = nullptr) {
   const int tid = threadIdx.x;
-  // diagnostic clocks (ppf_phase_profile): [0] brute force, [1] Nelder-Mead, [2] NM calls
+  // diagnostic clocks (ppf_phase_profile): [0] brute force, [1] Nelder-Mead, [2] NM calls,
+  // [3] prime-factor grids re-taken by direct sums
   const unsigned long long c0 = clk ? wall_clock64() : 0ull;
   // ---- brute force over the inclusive grid (np.mgrid[lo:hi:Ns*1j]) ----
   // grid and simplex arithmetic use explicit _rn ops: hipcc would otherwise
@@ -468,8 +548,10 @@ __device__ inline void guess_search(const double2* rm, int NH, double ie2, int N
     int A = 0, B = 0;
     const bool pfa = pfa_scr && allow_fold && lo == -0.5 && hi == 0.5 &&
                      pfa_scratch_slots(Ns, NH) > 0 && pfa_split(L, A, B);
-    if (!pfa || pfa_pass(rm, NH, ie2, Ns, lo, hi, gs, pfa_scr, A, B))
+    if (!pfa || pfa_pass(rm, NH, ie2, Ns, lo, hi, gs, pfa_scr, A, B, clk)) {
+      if (clk && pfa && tid == 0) atomicAdd(&clk[3], 1ull);  // [3] PFA near-tie re-takes
       brute_pass<false>(rm, NH, ie2, Ns, lo, hi, gs);
+    }
   }
   const unsigned long long c1 = clk ? wall_clock64() : 0ull;
   // ---- Nelder-Mead polish: every thread runs the (uniform, scalar) simplex
