@@ -329,10 +329,10 @@ __device__ inline bool pfa_pass(const double2* rm, int NH, double ie2, int Ns, d
                                 unsigned long long* clk = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   unsigned long long tc = clk ? wall_clock64() : 0ull;
-  auto tick = [&](int slot) {  // diagnostic: [4 + slot] phase clocks of this pass
-    if (clk && tid == 0) {
+  auto tick = [&](int slot) {  // diagnostic: [13 + slot] phase clocks of this pass
+    if (clk && tid == 0) {      // (ptime 23-25: clear of k_post's 16-22)
       const unsigned long long t = wall_clock64();
-      atomicAdd(&clk[4 + slot], t - tc);
+      atomicAdd(&clk[13 + slot], t - tc);
       tc = t;
     }
   };

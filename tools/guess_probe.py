@@ -45,8 +45,8 @@ def main(nsub=4096):
               "Nelder-Mead %.1f ms, %.1f NM calls per subint, %d grids re-taken directly; "
               "PFA setup / stage 1 / stage 2 %.1f / %.1f / %.1f ms; data pass %.3f ms, fit %.3f ms"
               % ("direct" if direct else "prime-factor", kt["guess"][0],
-                 clk[10] / 1e5, clk[11] / 1e5, clk[12] / nsub, clk[13], clk[14] / 1e5,
-                 clk[15] / 1e5, clk[16] / 1e5, kt["data_xspec"][0],
+                 clk[10] / 1e5, clk[11] / 1e5, clk[12] / nsub, clk[13], clk[23] / 1e5,
+                 clk[24] / 1e5, clk[25] / 1e5, kt["data_xspec"][0],
                  kt["fit_taylor"][0]))
     print("guesses identical:", bool(np.array_equal(res[False], res[True])),
           "max |d| %.3g" % np.max(np.abs(res[False] - res[True])))
