@@ -1162,6 +1162,10 @@ __global__ __launch_bounds__(64) void k_guess_w(FitArgs a) {
   const int NH = a.NH;
   const int midx = a.model_idx ? a.model_idx[s] : 0;
   const double2* Mm = a.Mmean + (size_t)midx * a.NHP;
+  // diagnostic clocks (ppf_phase_profile, lane 0): [10] set-up + brute
+  // force, [11] Nelder-Mead, [12] NM calls, [26] up to the fold sums, [27] up to rm
+  unsigned long long* clk = a.ptime ? a.ptime + 10 : nullptr;
+  const unsigned long long c0 = clk ? wall_clock64() : 0ull;
   double2 rm[kGwM];
   double pv[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -1174,6 +1178,7 @@ __global__ __launch_bounds__(64) void k_guess_w(FitArgs a) {
     }
   }
   const double pno = vsum4(pv);
+  if (clk && lane == 0) atomicAdd(&clk[17], wall_clock64() - c0);  // [27] set-up + rm
   const double noise = sqrt(pno / (double)a.nbin / (double)(NH - a.kc));
   const double err2 = noise * noise * (0.5 * (double)a.nbin);
   const double ie2 = 1.0 / err2;
@@ -1193,6 +1198,7 @@ __global__ __launch_bounds__(64) void k_guess_w(FitArgs a) {
     fw[t] = cmk(cs, sn);
   }
   __syncthreads();  // one wave: orders the LDS writes before the reads
+  if (clk && lane == 0) atomicAdd(&clk[16], wall_clock64() - c0);
   const int jm = (L + 1) / 2;
   double myf[2] = {NAN, NAN};
   double bv = NAN;
@@ -1255,6 +1261,7 @@ __global__ __launch_bounds__(64) void k_guess_w(FitArgs a) {
     wave_argmin(bv, bi);
   }
   const double x0 = (bi == Ns - 1) ? hi : __dadd_rn(__dmul_rn((double)bi, step), lo);
+  const unsigned long long c1 = clk ? wall_clock64() : 0ull;
   // ---- Nelder-Mead polish (guess_search) ----
   const int maxfun = 200, maxiter = 200;
   int fcalls = 0;
@@ -1303,6 +1310,11 @@ __global__ __launch_bounds__(64) void k_guess_w(FitArgs a) {
     if (f1 < f0) { double t = s0; s0 = s1; s1 = t; t = f0; f0 = f1; f1 = t; }
   }
   if (f1 < f0) { double t = s0; s0 = s1; s1 = t; }
+  if (clk && lane == 0) {
+    atomicAdd(&clk[0], c1 - c0);
+    atomicAdd(&clk[1], wall_clock64() - c1);
+    atomicAdd(&clk[2], (unsigned long long)fcalls);
+  }
   if (lane == 0) {
     double nug = a.guess_nu ? a.guess_nu[s] : NAN;
     if (isnan(nug)) nug = fmean;

@@ -67,8 +67,8 @@ print("phase clocks per workgroup (us):",
       {n: round(pt[i] / nwg / 100.0, 2) for i, n in
        enumerate(["moment pass (fused)", "meta+T0", "centre", "sweep", "trstep"])},
       "recentres/subint", pt[8] / nwg, "workgroups", pt[9],
-      "guess brute/NM us", round(pt[10] / nwg / 100.0, 2), round(pt[11] / nwg / 100.0, 2),
-      "NM calls", pt[12] / nwg)
+      "guess set-up+brute / NM us", round(pt[10] / nwg / 100.0, 2), round(pt[11] / nwg / 100.0, 2),
+      "(of which set-up + fold sums %.2f, set-up + rm %.2f)" % (pt[26] / nwg / 100.0, pt[27] / nwg / 100.0), "NM calls", pt[12] / nwg)
 
 # the fused kernel with one objective sweep and no solver steps (eval_only):
 # the moment pass + meta + one sweep, i.e. the streaming part alone
