@@ -47,6 +47,84 @@ def register_archive(name, bunch):
     return name
 
 
+class _Stack:
+    """Archives registered together (register_archives) with one subints
+    shape [nsub, npol, nchan, nbin]: their metadata arrays stacked on a
+    leading archive axis -- freqs / weights [narch, nsub, nchan], snrs0 and
+    noise0 (polarisation 0 of SNRs / noise_stds; noise0 NaN for the archives
+    without, has_noise [narch], None when none has them) [narch, nsub,
+    nchan], Ps [narch, nsub], DM [narch] --
+    each archive's bunch holding views of its own row, and ``rows`` one
+    [narch, nsub, npol, nchan, nbin] view of their subints when those are
+    equally spaced views of one tensor (else None).  allok: every archive's
+    ok_isubs is every subint and every ok_ichans every channel."""
+
+
+def _stacked_view(subs):
+    """One [narch, *shape] view of equally spaced tensors of one storage with
+    the same shape and strides, or None."""
+    t0 = subs[0]
+    if not _is_tensor(t0) or not t0.is_contiguous():
+        return None
+    shape, st0 = t0.shape, t0.stride()
+    base0 = t0._base
+    if base0 is None or not all(_is_tensor(t) and t._base is base0 and t.shape == shape and
+                                t.stride() == st0 for t in subs):
+        return None
+    q = np.fromiter((t.data_ptr() for t in subs), dtype=np.int64, count=len(subs))
+    es = t0.element_size()
+    d = int(q[1] - q[0]) if len(subs) > 1 else t0.numel() * es
+    if d < t0.numel() * es or d % es or (len(subs) > 2 and (np.diff(q) != d).any()):
+        return None
+    return t0.as_strided((len(subs),) + tuple(shape), (d // es,) + tuple(st0),
+                         t0.storage_offset())
+
+
+def register_archives(names, bunches):
+    """register_archive for many archives at once (a driver's whole data set
+    kept in memory, e.g. every archive ppalign aligns).  Each archive stays
+    loadable under its own name exactly as if registered alone; when they all
+    have one subints shape their metadata arrays are also stacked (_Stack), so
+    a driver that opens every one of them indexes one array per key instead
+    of visiting each archive (ppalign's unit set-up)."""
+    bs = [normalize(b, nm) for nm, b in zip(names, bunches)]
+    for nm, b in zip(names, bs):
+        _registry[nm] = b
+    if len(bs) < 2:
+        return list(names)
+    shape = tuple(bs[0].subints.shape)
+    if any(tuple(b.subints.shape) != shape for b in bs):
+        return list(names)
+    nsub, npol, nchan, nbin = shape
+    stk = _Stack()
+    stk.nsub, stk.npol, stk.nchan, stk.nbin = shape
+    try:
+        stk.freqs = np.stack([b.freqs for b in bs])
+        stk.weights = np.stack([b.weights for b in bs])
+        stk.snrs0 = np.stack([np.asarray(b.SNRs, dtype=np.float64)[:, 0] for b in bs])
+        stk.Ps = np.stack([b.Ps for b in bs])
+        stk.DM = np.array([float(b.DM) for b in bs])
+        stk.has_noise = np.array([b.noise_stds is not None for b in bs])
+        nan = np.full((nsub, nchan), np.nan)
+        stk.noise0 = np.stack([np.asarray(b.noise_stds, dtype=np.float64)[:, 0]
+                               if b.noise_stds is not None else nan for b in bs]) \
+            if stk.has_noise.any() else None
+    except (ValueError, IndexError, TypeError):
+        return list(names)
+    if stk.freqs.shape != (len(bs), nsub, nchan) or stk.weights.shape != stk.freqs.shape or \
+            stk.snrs0.shape != stk.freqs.shape or stk.Ps.shape != (len(bs), nsub):
+        return list(names)
+    full = np.arange(nsub)
+    stk.allok = all(len(b.ok_isubs) == nsub and np.array_equal(b.ok_isubs, full) and
+                    all(len(oi) == nchan for oi in b.ok_ichans) for b in bs)
+    stk.rows = _stacked_view([b.subints for b in bs])
+    for i, b in enumerate(bs):
+        # the bunch's own arrays become views of its stack row (equal values)
+        b.freqs, b.weights, b.Ps = stk.freqs[i], stk.weights[i], stk.Ps[i]
+        b["_stack"] = (stk, i)
+    return list(names)
+
+
 def unregister_archive(name):
     _registry.pop(name, None)
 
@@ -136,6 +214,7 @@ class _Registered:
         b = DataBunch()
         b.update(self.base)  # shallow copy (C-level), then drop the data
         b.pop("subints", None)
+        b.pop("_stack", None)  # register_archives' stack: registered views only
         return b
 
     def read(self, lo, hi):
@@ -411,9 +490,11 @@ def registered_view(filename, dedisperse=False, dededisperse=False, tscrunch=Fal
     b = _registry.get(filename) if isinstance(filename, str) else None
     if b is None:
         return None
-    dmc = int(b.get("dmc", 0))
-    if (dedisperse and not dmc) or (dededisperse and dmc) or (tscrunch and b.nsub > 1) or \
-            (rm_baseline and not b.get("baseline_removed", True)):
+    if dedisperse or dededisperse:  # would arch.dedisperse() / dededisperse() rotate?
+        dmc = int(b.get("dmc", 0))
+        if (dedisperse and not dmc) or (dededisperse and dmc):
+            return None
+    if (tscrunch and b.nsub > 1) or (rm_baseline and not b.get("baseline_removed", True)):
         return None
     return _RegisteredView(b)
 

@@ -52,20 +52,28 @@ def _open_all(datafiles, model_data, SNR_cutoff, quiet, skip_these, tscrunch, ps
     """Metadata of every archive (ppalign.py:121-159's checks, no DATA read):
     [(name, Archive)] of the archives to align."""
     out = []
+    # registered archives with nothing to process are read in place; with no
+    # tscrunch / baseline removal asked that is every registered one
+    reg = _arch._registry if not tscrunch and not rm_baseline else {}
+    RV = _arch._RegisteredView
+    nbin = model_data.nbin
     for name in datafiles:
-        try:  # ppalign.py:123-127 (rm_baseline False: F0_fact = 0, pptoas.py:26-29)
-            # a registered archive with nothing to process is read in place
-            a = _arch.registered_view(name, dedisperse=False, tscrunch=tscrunch,
-                                      rm_baseline=rm_baseline) or \
-                _arch.open_archive(name, dedisperse=False, tscrunch=tscrunch, pscrunch=pscrunch,
-                                   rm_baseline=rm_baseline, quiet=True)
-        except RuntimeError:
-            if not quiet:
-                print("%s: cannot load_data().  Skipping it." % name)
-            skip_these.append(name)
-            continue
+        b = reg.get(name) if isinstance(name, str) else None
+        if b is not None:
+            a = RV(b)
+        else:
+            try:  # ppalign.py:123-127 (rm_baseline False: F0_fact = 0, pptoas.py:26-29)
+                a = _arch.registered_view(name, dedisperse=False, tscrunch=tscrunch,
+                                          rm_baseline=rm_baseline) or \
+                    _arch.open_archive(name, dedisperse=False, tscrunch=tscrunch,
+                                       pscrunch=pscrunch, rm_baseline=rm_baseline, quiet=True)
+            except RuntimeError:
+                if not quiet:
+                    print("%s: cannot load_data().  Skipping it." % name)
+                skip_these.append(name)
+                continue
         m = a.meta
-        if m.nbin != model_data.nbin:
+        if m.nbin != nbin:
             if not quiet:
                 print("%s: %d != %d phase bins.  Skipping it." % (name, m.nbin, model_data.nbin))
             skip_these.append(name)
@@ -86,7 +94,123 @@ class _All(np.ndarray):
 ALL = None  # set per call: np.arange(nchan) viewed as _All
 
 
-def _units(opened, model_data):
+class _Bulk:
+    """Metadata of every opened archive stacked row-wise (one row per subint,
+    archives in order; archive i's rows are offs[i]:offs[i + 1]), so the unit
+    set-up indexes arrays instead of visiting 4,096 bunches one by one.  Built
+    only when every archive holds plain arrays of its own nsub rows and needs
+    nothing read to complete them (no snr_deferred); else ``build`` returns
+    None and the per-archive path runs.  Rows: F freqs, W weights, S SNRs of
+    polarisation 0, E noise_stds of polarisation 0 (NaN rows where an archive
+    has none; ``has_e`` says which rows have them), P periods, DM; ``same``
+    [narch]: every row of the archive equals the template's frequencies
+    (ppalign.py:156's freq_diffs all 0); ``regs`` [narch]: the registered
+    subints tensor of each archive or None; ``index``: name -> archive.
+    Archives registered together (archive.register_archives) are rows of one
+    stack already: their arrays are slices of it (no per-archive visit), with
+    ``allok`` (every channel of every subint on) and ``rows_view`` (every
+    row's [nchan, nbin] data as one view, npol 1) from the stack."""
+    allok = False
+    rows_view = None
+    unit_rows = None  # [nunits] bulk row of each unit (set by _units)
+
+    @staticmethod
+    def build(opened, model_data, nchan):
+        mfq = np.asarray(model_data.freqs)
+        if len(opened) == 0 or mfq.ndim != 2 or mfq.shape[0] != 1 or mfq.shape[1] != nchan:
+            return None
+        b = _Bulk._from_stack(opened, mfq, nchan)
+        if b is not None:
+            return b
+        metas = [a.meta for _, a in opened]
+        if any(m.get("snr_deferred") for m in metas):
+            return None
+        nsubs = [m.nsub for m in metas]
+        if min(nsubs) < 1:
+            return None
+        try:
+            F = np.concatenate([m.freqs for m in metas])
+            W = np.concatenate([m.weights for m in metas])
+            S = np.concatenate([np.asarray(m.SNRs)[:, 0] for m in metas])
+            P = np.concatenate([m.Ps for m in metas])
+        except (ValueError, IndexError, TypeError):
+            return None
+        offs = np.zeros(len(metas) + 1, dtype=np.int64)
+        np.cumsum(nsubs, out=offs[1:])
+        R = int(offs[-1])
+        if F.shape != (R, nchan) or W.shape != (R, nchan) or S.shape != (R, nchan) or \
+                P.shape != (R,) or F.dtype != np.float64:
+            return None
+        if [len(m.freqs) for m in metas] != nsubs:  # each archive's own rows
+            return None
+        b = _Bulk()
+        b.F, b.W, b.S, b.P, b.offs = F, W.astype(np.float64, copy=False), S, P, offs
+        b.DM = np.repeat(np.array([float(m.DM) for m in metas]), nsubs)
+        nss = [m.get("noise_stds") for m in metas]
+        b.has_e = np.repeat(np.array([ns is not None for ns in nss]), nsubs)
+        if b.has_e.all():
+            b.E = np.concatenate([np.asarray(ns)[:, 0] for ns in nss])
+        else:
+            b.E = np.full((R, nchan), np.nan)
+            for i, ns in enumerate(nss):
+                if ns is not None:
+                    b.E[offs[i]:offs[i + 1]] = np.asarray(ns)[:, 0]
+        # same frequencies as the template: freq_diffs all exactly 0 (NaN never)
+        b.same = np.logical_and.reduceat(((F - mfq) == 0.0).all(axis=1), offs[:-1])
+        b.regs = [a.registered_rows() for _, a in opened]
+        b.index = {name: i for i, (name, _) in enumerate(opened)}
+        return b
+
+    @staticmethod
+    def _from_stack(opened, mfq, nchan):
+        """build() for archives of one archive.register_archives stack, opened
+        as registered views: slices (or one fancy index) of the stack."""
+        RV = _arch._RegisteredView
+        if not all(type(a) is RV for _, a in opened):
+            return None
+        st = [a.meta.get("_stack") for _, a in opened]
+        s0 = st[0]
+        if s0 is None:
+            return None
+        stk = s0[0]
+        if not all(s is not None and s[0] is stk for s in st) or stk.nchan != nchan:
+            return None
+        idx = np.fromiter((s[1] for s in st), dtype=np.int64, count=len(st))
+        n = len(idx)
+        if n == 1 or (np.diff(idx) == 1).all():
+            sel = slice(int(idx[0]), int(idx[0]) + n)
+        else:
+            sel = idx
+        nsub = stk.nsub
+        R = n * nsub
+        b = _Bulk()
+        b.F = stk.freqs[sel].reshape(R, nchan)
+        b.W = stk.weights[sel].reshape(R, nchan)
+        b.S = stk.snrs0[sel].reshape(R, nchan)
+        b.P = stk.Ps[sel].reshape(R)
+        b.DM = np.repeat(stk.DM[sel], nsub)
+        b.offs = np.arange(n + 1, dtype=np.int64) * nsub
+        if stk.noise0 is not None:
+            b.E = stk.noise0[sel].reshape(R, nchan)
+            b.has_e = np.repeat(stk.has_noise[sel], nsub)
+        else:
+            b.E = None  # every row NaN
+            b.has_e = np.zeros(R, dtype=bool)
+        if np.isfinite(mfq).all():  # F - mfq == 0 exactly when F == mfq
+            eq = (b.F == mfq).all(axis=1)
+        else:
+            eq = ((b.F - mfq) == 0.0).all(axis=1)
+        b.same = eq.reshape(n, nsub).all(axis=1)
+        b.allok = stk.allok
+        if stk.rows is not None and stk.npol == 1:
+            b.rows_view = stk.rows[sel].reshape(R, nchan, stk.nbin)
+        b.regs = [a.meta.subints for _, a in opened]
+        b.index = {name: i for i, (name, _) in enumerate(opened)}
+        b.nsub = nsub
+        return b
+
+
+def _units(opened, model_data, bulk=None):
     """(name, subint, ichans, model_ichans) per ok subint (ppalign.py:153-177).
     A unit whose channels are all the template's (every channel on in both)
     carries the one shared index array ALL (its intersect1d)."""
@@ -96,6 +220,33 @@ def _units(opened, model_data):
     mok = model_data.ok_ichans[0]
     model_full = len(mok) == nch
     mfq = np.asarray(model_data.freqs)
+    if bulk is not None and model_full and bulk.allok and bulk.same.all():
+        # one register_archives stack, every channel on everywhere: every
+        # subint a unit with the shared ALL, in bulk row order
+        ns = bulk.nsub
+        units = [(name, isub, ALL, ALL) for name, _ in opened for isub in range(ns)]
+        bulk.unit_rows = np.arange(len(units), dtype=np.int64)
+        return units
+    if bulk is not None:
+        if model_full:  # the common case: rows of every channel, one shared ALL
+            for (name, a), same in zip(opened, bulk.same.tolist()):
+                m = a.meta
+                if same:
+                    oic = m.ok_ichans
+                    for isub in m.ok_isubs:
+                        isub = int(isub)
+                        oi = oic[isub]
+                        if len(oi) == nch:
+                            units.append((name, isub, ALL, ALL))
+                        else:
+                            ichans = np.intersect1d(oi, mok)
+                            units.append((name, isub, ichans, ichans))
+                else:
+                    _units_of(units, name, m, False, mf, mok, model_full)
+        else:
+            for (name, a), same in zip(opened, bulk.same.tolist()):
+                _units_of(units, name, a.meta, same, mf, mok, model_full)
+        return units
     mbytes = mfq.tobytes()
     for name, a in opened:
         m = a.meta
@@ -109,18 +260,25 @@ def _units(opened, model_data):
                 same = fd.min() == fd.max() == 0.0
             except ValueError:
                 same = False
-        for isub in m.ok_isubs:
-            if same:
-                oi = m.ok_ichans[isub]
-                if model_full and len(oi) == nch:  # ok_ichans are sorted, unique
-                    ichans = mich = ALL
-                else:
-                    ichans = np.intersect1d(oi, mok)
-                    mich = ichans
+        _units_of(units, name, m, same, mf, mok, model_full)
+    return units
+
+
+def _units_of(units, name, m, same, mf, mok, model_full):
+    """One archive's units (see _units); same: its frequencies are the template's."""
+    nch = len(mf)
+    for isub in m.ok_isubs:
+        if same:
+            oi = m.ok_ichans[isub]
+            if model_full and len(oi) == nch:  # ok_ichans are sorted, unique
+                ichans = mich = ALL
             else:
-                ichans = np.asarray(m.ok_ichans[isub])
-                mich = np.array([np.argmin(abs(mf - m.freqs[isub, c])) for c in ichans])
-            units.append((name, int(isub), ichans, mich))
+                ichans = np.intersect1d(oi, mok)
+                mich = ichans
+        else:
+            ichans = np.asarray(m.ok_ichans[isub])
+            mich = np.array([np.argmin(abs(mf - m.freqs[isub, c])) for c in ichans])
+        units.append((name, int(isub), ichans, mich))
     return units
 
 
@@ -153,38 +311,32 @@ def _strided_rows(rows):
     t0, j0 = rows[0]
     if t0.dim() != 4 or t0.shape[1] != 1 or t0.dtype != torch.float64:
         return None
-    shape = t0.shape[1:]
-    nchan, nbin = shape[1], shape[2]
-    # one storage: every row a view of t0's base (a cheap identity test), or
-    # failing that the storages' own addresses
-    base0 = t0._base
-    sbase = None if base0 is not None else t0.untyped_storage().data_ptr()
+    shape = t0.shape
+    nchan, nbin = shape[2], shape[3]
     st0 = t0.stride()
     if (nbin > 1 and st0[3] != 1) or (nchan > 1 and st0[2] != nbin):
         return None
-    p0 = t0.data_ptr() + j0 * st0[0] * 8
-    if len(rows) > 1:
-        t1, j1 = rows[1]
-        st = t1.data_ptr() + j1 * t1.stride(0) * 8 - p0
-    else:
-        st = nchan * nbin * 8
-    if st < nchan * nbin * 8 or st % 8:
-        return None
-    p = p0
-    for t, j in rows:
-        if t is not t0:
-            if (t._base is not base0 if base0 is not None else
-                    t.untyped_storage().data_ptr() != sbase) or t.shape[1:] != shape:
-                return None
-            stt = t.stride()
-            if stt[2:] != st0[2:]:
-                return None
-            q = t.data_ptr() + j * stt[0] * 8
-        else:
-            q = t.data_ptr() + j * st0[0] * 8
-        if q != p:
+    # one storage: every row a view of t0's base (a cheap identity test), or
+    # failing that the storages' own addresses; the same [1, nchan, nbin] row
+    # shape and channel / bin strides (tested per distinct tensor: archives
+    # may share one)
+    base0 = t0._base
+    ts = {id(t): t for t, _ in rows}.values() if len(rows) > 1 else (t0,)
+    if base0 is not None:
+        if not all(t._base is base0 for t in ts):
             return None
-        p += st
+    else:
+        sbase = t0.untyped_storage().data_ptr()
+        if not all(t.untyped_storage().data_ptr() == sbase for t in ts):
+            return None
+    if not all(t.shape[1:] == shape[1:] and t.stride()[2:] == st0[2:] for t in ts):
+        return None
+    # the rows' addresses, equally spaced by st bytes
+    q = np.fromiter((t.data_ptr() + j * t.stride(0) * 8 for t, j in rows), dtype=np.int64,
+                    count=len(rows))
+    st = int(q[1] - q[0]) if len(rows) > 1 else nchan * nbin * 8
+    if st < nchan * nbin * 8 or st % 8 or (len(rows) > 2 and (np.diff(q) != st).any()):
+        return None
     off = t0.storage_offset() + j0 * st0[0]
     return t0.as_strided((len(rows), nchan, nbin), (st // 8, nbin, 1), off)
 
@@ -199,12 +351,15 @@ class _UnitStack:
     rows of one tensor -- and their host arrays stacked row-wise; the others
     take the per-channel path."""
 
-    def __init__(self, eng, units, opened, model_freqs, npol, nchan, nbin):
+    def __init__(self, eng, units, opened, model_freqs, npol, nchan, nbin, bulk=None,
+                 urows=None):
         dev = eng.device
         n = len(units)
         f64 = dict(dtype=torch.float64, device=dev)
         self.n = n
         self.pols = [None] * npol
+        if bulk is not None and npol == 1 and self._from_bulk(dev, units, bulk, urows):
+            return
         freqs = np.tile(np.asarray(model_freqs, dtype=np.float64), (n, 1))
         errs = np.ones((n, nchan))
         mask = np.zeros((n, nchan), dtype=np.uint8)
@@ -305,6 +460,47 @@ class _UnitStack:
         self.freqs, self.errs, self.mask, self.wts = freqs, errs, mask, wts
         self.P, self.DMg, self.nu_fit = P, DMg, nu_fit
 
+    def _from_bulk(self, dev, units, bulk, urows=None):
+        """The same stack when every unit is full (ALL) and every archive is
+        registered: its host arrays are rows of the stacked metadata (one
+        fancy index each), its data one strided view of the registered rows
+        (or one gather).  urows: the bulk rows of these units when the caller
+        has them (_units' unit_rows).  False (nothing set) when that does not
+        apply."""
+        if urows is not None and bulk.rows_view is not None:
+            rows = urows  # one register_archives stack: every unit full
+            n = len(rows)
+            if n and rows[-1] - rows[0] == n - 1 and (n < 3 or (np.diff(rows) == 1).all()):
+                rows = slice(int(rows[0]), int(rows[0]) + n)  # views, no copies
+                view = bulk.rows_view[rows]
+            else:
+                view = bulk.rows_view[torch.as_tensor(rows, device=bulk.rows_view.device)]
+            if view.device != dev:
+                view = view.to(dev)
+        else:
+            if not all(type(u[2]) is _All for u in units):
+                return False
+            ix, regs = bulk.index, bulk.regs
+            ai = [ix[u[0]] for u in units]
+            src = [(regs[i], u[1]) for i, u in zip(ai, units)]
+            if any(not isinstance(t, torch.Tensor) for t, _ in src):
+                return False
+            rows = bulk.offs[np.array(ai, dtype=np.int64)] + \
+                np.fromiter((u[1] for u in units), dtype=np.int64, count=len(units))
+            view = _strided_rows(src)
+            if view is None:
+                view = torch.stack([t[j, 0] for t, j in src]).to(dev)
+        freqs = bulk.F[rows]
+        # NaN rows: the data pass estimates them (see __init__)
+        errs = torch.full(freqs.shape, float("nan"), dtype=torch.float64, device=dev) \
+            if bulk.E is None else bulk.E[rows]
+        self.pols = [view]
+        self.freqs, self.errs, self.wts = freqs, errs, bulk.W[rows]
+        self.mask = np.ones(freqs.shape, dtype=np.uint8)
+        self.P, self.DMg = bulk.P[rows], bulk.DM[rows]
+        self.nu_fit = _guess_fit_freq_rows(freqs, bulk.S[rows])
+        return True
+
     def fit_and_accumulate(self, eng, model_port, fit_dm, accum, tw, mark=None):
         """One iteration's fits (ppalign.py:178-195) and weighted rotate-and-sum
         (ppalign.py:202-208) in the Fourier domain.  The fit results stay on
@@ -396,14 +592,19 @@ def align_archives(metafile, initial_guess, fit_dm=True, tscrunch=False, pscrunc
     opened = _open_all(datafiles, model_data, SNR_cutoff, quiet, skip_these, tscrunch, pscrunch)
     global ALL
     ALL = np.arange(nchan).view(_All)
-    units = _units(opened, model_data)
+    bulk = _Bulk.build(opened, model_data, nchan)
+    units = _units(opened, model_data, bulk)
     t0 = mark("open", t0)
     lo, hi = shard_range(len(units), rank, world)
     mine = units[lo:hi]
     multi = [u for u in mine if len(u[2]) > 1]
     single = [u for u in mine if len(u[2]) <= 1]
-    stack = _UnitStack(eng, multi, opened, model_data.freqs[0], npol, nchan, nbin) \
-        if multi else None
+    # bulk rows of this rank's units when _units made them in bulk order
+    urows = bulk.unit_rows[lo:hi] if bulk is not None and bulk.unit_rows is not None and \
+        not single else None
+    stack = _UnitStack(eng, multi, opened, model_data.freqs[0], npol, nchan, nbin, bulk,
+                       urows) if multi else None
+    del bulk
     t0 = mark("unit_stack", t0)
     archives = {}
     for name, a in opened:  # 1-channel hack units (rare): their archives on the host
