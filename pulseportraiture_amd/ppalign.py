@@ -9,6 +9,8 @@ the only collective is one all-reduce (sum, fp64) of the [nchan, nbin/2+1]
 spectrum and the channel weights per iteration -- RCCL over xGMI with the
 "nccl" backend.  Every rank then divides locally and holds the new template.
 """
+import gc
+
 import numpy as np
 import torch
 
@@ -589,22 +591,32 @@ def align_archives(metafile, initial_guess, fit_dm=True, tscrunch=False, pscrunc
     dev = eng.device
     rank, world = dist_info()
     skip_these = []
-    opened = _open_all(datafiles, model_data, SNR_cutoff, quiet, skip_these, tscrunch, pscrunch)
-    global ALL
-    ALL = np.arange(nchan).view(_All)
-    bulk = _Bulk.build(opened, model_data, nchan)
-    units = _units(opened, model_data, bulk)
-    t0 = mark("open", t0)
-    lo, hi = shard_range(len(units), rank, world)
-    mine = units[lo:hi]
-    multi = [u for u in mine if len(u[2]) > 1]
-    single = [u for u in mine if len(u[2]) <= 1]
-    # bulk rows of this rank's units when _units made them in bulk order
-    urows = bulk.unit_rows[lo:hi] if bulk is not None and bulk.unit_rows is not None and \
-        not single else None
-    stack = _UnitStack(eng, multi, opened, model_data.freqs[0], npol, nchan, nbin, bulk,
-                       urows) if multi else None
-    del bulk
+    # a few objects per archive and unit, none cyclic: keep the cyclic
+    # collector (a full pass over every live object, tens of ms with 4,096
+    # registered archives) out of the set-up
+    gc_on = gc.isenabled()
+    gc.disable()
+    try:
+        opened = _open_all(datafiles, model_data, SNR_cutoff, quiet, skip_these, tscrunch,
+                           pscrunch)
+        global ALL
+        ALL = np.arange(nchan).view(_All)
+        bulk = _Bulk.build(opened, model_data, nchan)
+        units = _units(opened, model_data, bulk)
+        t0 = mark("open", t0)
+        lo, hi = shard_range(len(units), rank, world)
+        mine = units[lo:hi]
+        multi = [u for u in mine if len(u[2]) > 1]
+        single = [u for u in mine if len(u[2]) <= 1]
+        # bulk rows of this rank's units when _units made them in bulk order
+        urows = bulk.unit_rows[lo:hi] if bulk is not None and bulk.unit_rows is not None and \
+            not single else None
+        stack = _UnitStack(eng, multi, opened, model_data.freqs[0], npol, nchan, nbin, bulk,
+                           urows) if multi else None
+        del bulk
+    finally:
+        if gc_on:
+            gc.enable()
     t0 = mark("unit_stack", t0)
     archives = {}
     for name, a in opened:  # 1-channel hack units (rare): their archives on the host

@@ -1,6 +1,7 @@
 """Wall time of consecutive align_archives calls at config 5 (the bench
 leg's set-up), each with its phase split: does a call's time depend on its
 position after the warm-up?"""
+import gc
 import os
 import sys
 import time
@@ -27,13 +28,24 @@ def main():
                                       for i in range(narch)])
     archive.register_archive("pc_guess", dict(subints=w.model[None, None], freqs=w.freqs,
                                               Ps=[w.P], epochs=[(57000, 0, 0.0)], DM=w.DM0, dmc=1))
+    gct = {"n2": 0, "t2": 0.0, "t": 0.0}
+
+    def cb(phase, info):  # full (generation 2) collections and their time
+        if phase == "start":
+            gct["t"] = time.perf_counter()
+        elif info["generation"] == 2:
+            gct["n2"] += 1
+            gct["t2"] += time.perf_counter() - gct["t"]
+    gc.callbacks.append(cb)
     for k in range(6):
+        gct["n2"], gct["t2"] = 0, 0.0
         ph = {} if k >= 3 else None
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         ppalign.align_archives(names, "pc_guess", fit_dm=True, niter=3, quiet=True, timings=ph)
         torch.cuda.synchronize()
-        print("call %d: %.1f ms %s" % (k, (time.perf_counter() - t0) * 1e3,
+        print("call %d: %.1f ms (gen-2 collections %d, %.1f ms) %s" % (
+            k, (time.perf_counter() - t0) * 1e3, gct["n2"], gct["t2"] * 1e3,
                                        "" if ph is None else
                                        {a: round(b * 1e3, 1) for a, b in ph.items()}), flush=True)
 
