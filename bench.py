@@ -92,8 +92,8 @@ def pmc_traffic(kernel, nsub, config, per_step=False):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="headline", choices=sorted(CONFIGS))
     ap.add_argument("--nsub", type=int, default=None, help="subints per GPU (override)")
     ap.add_argument("--seed", type=int, default=20240917)
