@@ -1115,7 +1115,7 @@ __device__ double row_eval_phase_g(const FitArgs& a, const double2* Rr, const do
   return acc;
 }
 
-__global__ __launch_bounds__(64) void k_guess_w(FitArgs a) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_guess_w(FitArgs a) {
   __shared__ double2 fb[kBlock / 2], fw[kBlock / 2];
   const int c = blockIdx.x, s = a.sub0 + c, lane = threadIdx.x;
   if (!guess_wave_ok(a, s)) return;
