@@ -1115,7 +1115,7 @@ __device__ double row_eval_phase_g(const FitArgs& a, const double2* Rr, const do
   return acc;
 }
 
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_guess_w(FitArgs a) {
+__global__ __launch_bounds__(64) void k_guess_w(FitArgs a) {
   __shared__ double2 fb[kBlock / 2], fw[kBlock / 2];
   const int c = blockIdx.x, s = a.sub0 + c, lane = threadIdx.x;
   if (!guess_wave_ok(a, s)) return;
@@ -1263,7 +1263,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
   const double x0 = (bi == Ns - 1) ? hi : __dadd_rn(__dmul_rn((double)bi, step), lo);
   const unsigned long long c1 = clk ? wall_clock64() : 0ull;
   // ---- Nelder-Mead polish (guess_search) ----
-  const int maxfun = 200, maxiter = 200;
+  const int maxfun = 200;
   int fcalls = 0;
   bool stop = false;
   auto F = [&](double xv) -> double {
@@ -1271,45 +1271,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
     ++fcalls;
     return -wave_eval_phase(rm, NH, xv, lane) * ie2;
   };
-  double s0 = x0;
-  double s1 = (s0 != 0.0) ? (1.0 + 0.05) * s0 : 0.00025;
-  double f0 = F(s0), f1 = F(s1);
-  if (f1 < f0) { double t = s0; s0 = s1; s1 = t; t = f0; f0 = f1; f1 = t; }
-  int it = 1;
-  while (fcalls < maxfun && it < maxiter) {
-    if (fabs(s1 - s0) <= 1e-4 && fabs(f0 - f1) <= 1e-4) break;
-    const double xbar = s0;
-    const double xr = __dsub_rn(__dmul_rn(2.0, xbar), s1);
-    const double fxr = F(xr);
-    if (stop) break;
-    bool shrink = false;
-    if (fxr < f0) {
-      const double xe = __dsub_rn(__dmul_rn(3.0, xbar), __dmul_rn(2.0, s1));
-      const double fxe = F(xe);
-      if (stop) break;
-      if (fxe < fxr) { s1 = xe; f1 = fxe; } else { s1 = xr; f1 = fxr; }
-    } else {
-      if (fxr < f1) {
-        const double xc = __dsub_rn(__dmul_rn(1.5, xbar), __dmul_rn(0.5, s1));
-        const double fxc = F(xc);
-        if (stop) break;
-        if (fxc <= fxr) { s1 = xc; f1 = fxc; } else shrink = true;
-      } else {
-        const double xcc = __dadd_rn(__dmul_rn(0.5, xbar), __dmul_rn(0.5, s1));
-        const double fxcc = F(xcc);
-        if (stop) break;
-        if (fxcc < f1) { s1 = xcc; f1 = fxcc; } else shrink = true;
-      }
-      if (shrink) {
-        s1 = __dadd_rn(s0, __dmul_rn(0.5, __dsub_rn(s1, s0)));
-        f1 = F(s1);
-        if (stop) break;
-      }
-    }
-    ++it;
-    if (f1 < f0) { double t = s0; s0 = s1; s1 = t; t = f0; f0 = f1; f1 = t; }
-  }
-  if (f1 < f0) { double t = s0; s0 = s1; s1 = t; }
+  double s0, f0, s1, f1;
+  nm_polish(F, stop, fcalls, maxfun, x0, s0, f0, s1, f1);
   if (clk && lane == 0) {
     atomicAdd(&clk[0], c1 - c0);
     atomicAdd(&clk[1], wall_clock64() - c1);

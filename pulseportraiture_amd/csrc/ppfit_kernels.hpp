@@ -498,6 +498,84 @@ __device__ inline bool pfa_pass(const double2* rm, int NH, double ie2, int Ns, d
   return __syncthreads_or(near);
 }
 
+// scipy.optimize.fmin's simplex moves in one variable (guess_search's
+// polish, maxiter 200, xtol = ftol = 1e-4): F(x) evaluates and counts (it
+// sets stop instead once maxfun calls are spent); on return (s0, f0) is the
+// best vertex and (s1, f1) the other.  Written as a state machine around ONE
+// call of F, so the evaluation (a block- or wave-wide phasor sum) is inlined
+// once instead of at each of the seven moves.  stt names the point xv being
+// evaluated: 0 s0, 1 s1 (the start), 2 reflection, 3 expansion, 4 outside
+// contraction, 5 inside contraction, 6 shrink.
+template <class Eval>
+__device__ __forceinline__ void nm_polish(Eval& F, const bool& stop, const int& fcalls,
+                                          int maxfun, double x0, double& s0, double& f0,
+                                          double& s1, double& f1) {
+  const int maxiter = 200;
+  s0 = x0;
+  s1 = (s0 != 0.0) ? (1.0 + 0.05) * s0 : 0.00025;
+  f0 = 0.0;
+  f1 = 0.0;
+  double fxr = 0.0, xr = 0.0, xv = s0;
+  int it = 1;
+  int stt = 0;
+  for (;;) {
+    const double fv = F(xv);
+    if (stop) break;
+    bool moved = false;  // an iteration's move is complete
+    if (stt == 0) {
+      f0 = fv;
+      xv = s1;
+      stt = 1;
+      continue;
+    } else if (stt == 1) {
+      f1 = fv;
+      if (f1 < f0) { double t = s0; s0 = s1; s1 = t; t = f0; f0 = f1; f1 = t; }
+    } else if (stt == 2) {
+      fxr = fv;
+      xr = xv;
+      const double xbar = s0;
+      if (fxr < f0) {
+        xv = __dsub_rn(__dmul_rn(3.0, xbar), __dmul_rn(2.0, s1));
+        stt = 3;
+      } else if (fxr < f1) {
+        xv = __dsub_rn(__dmul_rn(1.5, xbar), __dmul_rn(0.5, s1));
+        stt = 4;
+      } else {
+        xv = __dadd_rn(__dmul_rn(0.5, xbar), __dmul_rn(0.5, s1));
+        stt = 5;
+      }
+      continue;
+    } else if (stt == 3) {
+      if (fv < fxr) { s1 = xv; f1 = fv; } else { s1 = xr; f1 = fxr; }
+      moved = true;
+    } else if (stt == 4 || stt == 5) {
+      if (stt == 4 ? (fv <= fxr) : (fv < f1)) {
+        s1 = xv;
+        f1 = fv;
+        moved = true;
+      } else {  // shrink toward the best vertex
+        s1 = __dadd_rn(s0, __dmul_rn(0.5, __dsub_rn(s1, s0)));
+        xv = s1;
+        stt = 6;
+        continue;
+      }
+    } else {
+      f1 = fv;
+      moved = true;
+    }
+    if (moved) {
+      ++it;
+      if (f1 < f0) { double t = s0; s0 = s1; s1 = t; t = f0; f0 = f1; f1 = t; }
+    }
+    // the next iteration: loop condition, convergence test, reflection
+    if (!(fcalls < maxfun && it < maxiter)) break;
+    if (fabs(s1 - s0) <= 1e-4 && fabs(f0 - f1) <= 1e-4) break;
+    xv = __dsub_rn(__dmul_rn(2.0, s0), s1);
+    stt = 2;
+  }
+  if (f1 < f0) { double t = s0; s0 = s1; s1 = t; t = f0; f0 = f1; f1 = t; }
+}
+
 __device__ inline void guess_search(const double2* rm, int NH, double ie2, int Ns, double lo,
                                     double hi, GuessShared& gs, bool allow_fold = true,
                                     unsigned long long* clk = nullptr,
@@ -557,7 +635,7 @@ __device__ inline void guess_search(const double2* rm, int NH, double ie2, int N
   // ---- Nelder-Mead polish: every thread runs the (uniform, scalar) simplex
   // logic; each evaluation is one block-wide sum ----
   {
-    const int maxfun = 200, maxiter = 200;
+    const int maxfun = 200;
     int fcalls = 0;
     bool stop = false;
     auto F = [&](double xv) -> double {
@@ -565,45 +643,8 @@ __device__ inline void guess_search(const double2* rm, int NH, double ie2, int N
       ++fcalls;
       return -block_eval_phase(rm, NH, xv, gs.ev[fcalls & 1]) * ie2;
     };
-    double s0 = gs.x0;
-    double s1 = (s0 != 0.0) ? (1.0 + 0.05) * s0 : 0.00025;
-    double f0 = F(s0), f1 = F(s1);
-    if (f1 < f0) { double t = s0; s0 = s1; s1 = t; t = f0; f0 = f1; f1 = t; }
-    int it = 1;
-    while (fcalls < maxfun && it < maxiter) {
-      if (fabs(s1 - s0) <= 1e-4 && fabs(f0 - f1) <= 1e-4) break;
-      const double xbar = s0;
-      const double xr = __dsub_rn(__dmul_rn(2.0, xbar), s1);
-      const double fxr = F(xr);
-      if (stop) break;
-      bool shrink = false;
-      if (fxr < f0) {
-        const double xe = __dsub_rn(__dmul_rn(3.0, xbar), __dmul_rn(2.0, s1));
-        const double fxe = F(xe);
-        if (stop) break;
-        if (fxe < fxr) { s1 = xe; f1 = fxe; } else { s1 = xr; f1 = fxr; }
-      } else {
-        if (fxr < f1) {
-          const double xc = __dsub_rn(__dmul_rn(1.5, xbar), __dmul_rn(0.5, s1));
-          const double fxc = F(xc);
-          if (stop) break;
-          if (fxc <= fxr) { s1 = xc; f1 = fxc; } else shrink = true;
-        } else {
-          const double xcc = __dadd_rn(__dmul_rn(0.5, xbar), __dmul_rn(0.5, s1));
-          const double fxcc = F(xcc);
-          if (stop) break;
-          if (fxcc < f1) { s1 = xcc; f1 = fxcc; } else shrink = true;
-        }
-        if (shrink) {
-          s1 = __dadd_rn(s0, __dmul_rn(0.5, __dsub_rn(s1, s0)));
-          f1 = F(s1);
-          if (stop) break;
-        }
-      }
-      ++it;
-      if (f1 < f0) { double t = s0; s0 = s1; s1 = t; t = f0; f0 = f1; f1 = t; }
-    }
-    if (f1 < f0) { double t = s0; s0 = s1; s1 = t; t = f0; f0 = f1; f1 = t; }
+    double s0, f0, s1, f1;
+    nm_polish(F, stop, fcalls, maxfun, gs.x0, s0, f0, s1, f1);
     if (tid == 0) {
       gs.x = s0;
       gs.fx = fmin(f0, f1);
