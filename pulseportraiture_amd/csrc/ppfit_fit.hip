@@ -2329,9 +2329,10 @@ __device__ void post_subint(const FitArgs& a, int c, int s, unsigned char* dyn, 
   if (prof && tid == 0) atomicAdd(&a.ptime[22], 1ull);
 }
 
-// Phase-family post-fit: capped at 128 VGPRs for four waves per SIMD (its
-// serial thread-0 sections are latency-bound; 1.16 -> 1.00 ms at config 2
-// despite the spills).  The scattering variant keeps its registers.
+// Phase-family post-fit: two workgroups per CU as the launch bound, which
+// the compiler meets with 168 VGPRs (three waves per SIMD, no spills).  r04
+// A/B at config 2: four per CU (128 VGPRs, 77 spilled) 0.47 -> 0.56 ms (r02's
+// code had preferred the cap).  The scattering variant keeps its registers.
 template <bool SCAT>
 __global__ __launch_bounds__(kBlock, SCAT ? 1 : PPF_POST_WG_PER_CU) void k_post(FitArgs a) {
   extern __shared__ __align__(16) unsigned char dyn[];
