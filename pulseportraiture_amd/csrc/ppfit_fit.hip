@@ -2077,13 +2077,14 @@ template <bool SCAT>
 __device__ void post_subint(const FitArgs& a, int c, int s, unsigned char* dyn, PostShared& sh) {
   const int tid = threadIdx.x;
   const int nchan = a.nchan;
-  // diagnostic phase clock (ppf_phase_profile): thread 0 only
+  // diagnostic phase clock (ppf_phase_profile): thread 0 adds; the clock is
+  // wave-uniform (scalar registers, see k_fit_taylor)
   const bool prof = a.ptime != nullptr;
   unsigned long long t0 = prof ? wall_clock64() : 0ull;
   auto mark = [&](int i) {
-    if (prof && tid == 0) {
+    if (prof) {
       const unsigned long long t1 = wall_clock64();
-      atomicAdd(&a.ptime[i], t1 - t0);
+      if (tid == 0) atomicAdd(&a.ptime[i], t1 - t0);
       t0 = t1;
     }
   };

@@ -309,6 +309,13 @@ struct TaylorShared {
   double ifact[kMT];  // c_inv_fact for taylor_cells
   int done, nok, slot, tslot, q, mvalid;
   int same;  // the proposal repeats the last evaluated point (same_point8)
+  // wave 0's solver state between its steps (per lane: gradient, point, last
+  // evaluated point, step and Hessian row; uniform scalars once): parked here
+  // across the sweeps every wave runs, so that those registers serve the
+  // sweeps instead of spilling them
+  double sv_g[64], sv_xl[64], sv_xe[64], sv_pl[64], sv_H[5][64];
+  double sv_f, sv_tr, sv_predv;
+  int sv_hits, sv_k, sv_status, sv_nfev;
 };
 
 // T slot 0 of subint c into the kernel's LDS copy (all threads; the caller
@@ -358,15 +365,15 @@ __global__ __launch_bounds__(kBlock, 3) void k_fit_taylor(FitArgs a) {
   const int c = blockIdx.x, s = a.sub0 + c, tid = threadIdx.x;
   const int lane = tid & 63;
   if (!fused_taylor(a, s)) return;
-  // diagnostic phase clock (ppf_phase_profile): thread 0 only
+  // diagnostic phase clock (ppf_phase_profile): thread 0 adds each phase's
+  // time straight into ptime; the clock itself is wave-uniform (scalar
+  // registers), so nothing of the profiler stays live in vector registers
   const bool prof = a.ptime != nullptr;
   unsigned long long t0 = prof ? wall_clock64() : 0ull;
-  unsigned long long pt[5] = {0, 0, 0, 0, 0};
-  unsigned long long nrc = 0;
   auto mark = [&](int i) {
-    if (prof && tid == 0) {
+    if (prof) {
       const unsigned long long t1 = wall_clock64();
-      pt[i] += t1 - t0;
+      if (tid == 0) atomicAdd(&a.ptime[i], t1 - t0);
       t0 = t1;
     }
   };
@@ -414,6 +421,39 @@ __global__ __launch_bounds__(kBlock, 3) void k_fit_taylor(FitArgs a) {
   double tr = 1.0, predv = 0.0, pl = 0.0;
   int hits = 0, k = 0, status = (m.nok == 0) ? -1 : 0, nfev = 0;
   double xe = 0.0;  // lane i < 5: the last evaluated point
+  auto save = [&] {  // wave 0
+    sh.sv_g[lane] = g;
+    sh.sv_xl[lane] = xl;
+    sh.sv_xe[lane] = xe;
+    sh.sv_pl[lane] = pl;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) sh.sv_H[j][lane] = Hrow[j];
+    if (lane == 0) {
+      sh.sv_f = f;
+      sh.sv_tr = tr;
+      sh.sv_predv = predv;
+      sh.sv_hits = hits;
+      sh.sv_k = k;
+      sh.sv_status = status;
+      sh.sv_nfev = nfev;
+    }
+  };
+  auto restore = [&] {  // wave 0, after the barrier that follows its save
+    g = sh.sv_g[lane];
+    xl = sh.sv_xl[lane];
+    xe = sh.sv_xe[lane];
+    pl = sh.sv_pl[lane];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) Hrow[j] = sh.sv_H[j][lane];
+    f = sh.sv_f;
+    tr = sh.sv_tr;
+    predv = sh.sv_predv;
+    hits = sh.sv_hits;
+    k = sh.sv_k;
+    status = sh.sv_status;
+    nfev = sh.sv_nfev;
+  };
+  if (tid < 64) save();
   auto load_fgh = [&](double& ff, double& gg, double (&HH)[5]) {
     ff = sh.out[0];
     gg = lane < 5 ? sh.out[1 + lane] : 0.0;
@@ -443,7 +483,7 @@ __global__ __launch_bounds__(kBlock, 3) void k_fit_taylor(FitArgs a) {
   // no stored centre covers p: p itself becomes one (one more X pass)
   auto recentre = [&](const double* p) -> int {
     const int wsl = sh.tslot ^ 1;
-    ++nrc;
+    if (prof && tid == 0) atomicAdd(&a.ptime[8], 1ull);  // recentres
     if (tid == 0) {
       st.mvalid &= ~(1 << wsl);
       sh.mvalid = st.mvalid;
@@ -487,12 +527,14 @@ __global__ __launch_bounds__(kBlock, 3) void k_fit_taylor(FitArgs a) {
         status = 1;
         if (lane == 0) sh.done = 1;
       }
+      save();
     }
     if (tid == 0) sh.tslot = q;
   }
   __syncthreads();
   while (!sh.done) {
     if (tid < 64) {
+      restore();
       const double jm = sqrt(dot8(g, g));
       if (!(jm >= -1.0)) {  // NaN gradient: scipy's loop condition fails
         status = 0;
@@ -509,6 +551,7 @@ __global__ __launch_bounds__(kBlock, 3) void k_fit_taylor(FitArgs a) {
           sh.same = same;
         }
       }
+      save();
     }
     __syncthreads();
     mark(4);
@@ -523,6 +566,7 @@ __global__ __launch_bounds__(kBlock, 3) void k_fit_taylor(FitArgs a) {
     if (fresh) sweep<0, false>(a, m, c, s, sh.xp, refs, P, sl, sh.out, sh.red, source(q));
     mark(3);
     if (tid < 64) {
+      restore();
       double fp, gp, Hp[5] = {0, 0, 0, 0, 0};
       load_fgh(fp, gp, Hp);
       if (fresh) {
@@ -554,9 +598,11 @@ __global__ __launch_bounds__(kBlock, 3) void k_fit_taylor(FitArgs a) {
           if (lane == 0) sh.done = 1;
         }
       }
+      save();
     }
     __syncthreads();
   }
+  if (tid < 64) restore();
   if (tid < 5) st.x[tid] = sh.x[tid];
   if (tid < 5) store_grad_hess(a, s, lane, m.nok > 0, g, Hrow);
   if (tid == 0) {
@@ -567,12 +613,7 @@ __global__ __launch_bounds__(kBlock, 3) void k_fit_taylor(FitArgs a) {
     st.xslot = sh.tslot;
     st.fin = 1;
     st.scat_post = false;
-    if (prof) {
-#pragma unroll
-      for (int i = 0; i < 5; ++i) atomicAdd(&a.ptime[i], pt[i]);
-      atomicAdd(&a.ptime[8], nrc);
-      atomicAdd(&a.ptime[9], 1ull);
-    }
+    if (prof) atomicAdd(&a.ptime[9], 1ull);
   }
 }
 
