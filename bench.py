@@ -60,7 +60,7 @@ FP64_PEAK_TFLOPS = 78.6  # AMD MI355X spec, fp64 vector = fp64 matrix (not in th
 # HBM bytes per launch per kernel from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
 # passes over this same bench (tools/profile_r03.sh + tools/pmc_summary.py)
 PMC_TRAFFIC = {c: os.path.join(ROOT, "profiles", "%s_pmc_traffic_%s.json" % (r, c))
-               for c, r in (("headline", "r04f"), ("scattering", "r04c"), ("gm", "r04c"),
+               for c, r in (("headline", "r04g"), ("scattering", "r04c"), ("gm", "r04c"),
                             ("ppalign", "r04e"))}
 KERNEL_SYMBOL = {"solve": "k_scat_sweep", "data_xspec": "k_data_xspec<10>",
                  "rot_accum": "k_rot_accum_w",
