@@ -120,3 +120,31 @@ def test_register_archives_stack_views():
     finally:
         for nm in names:
             archive.unregister_archive(nm)
+
+
+def test_register_archives_mixed_shapes_register_each():
+    """Archives of different subint counts are still each registered (no
+    stack); the set-up then takes the per-archive stacked path and agrees
+    with the per-archive one."""
+    rng = np.random.default_rng(11)
+    names = ["mx_%d" % i for i in range(3)]
+    bs = _bunches(3, "noise", rng)
+    bs[1] = dict(bs[1], subints=bs[1]["subints"][:1], Ps=bs[1]["Ps"][:1],
+                 epochs=bs[1]["epochs"][:1], SNRs=bs[1]["SNRs"][:1])  # one subint
+    archive.register_archives(names, bs)
+    archive.register_archive("mx_guess", dict(subints=np.zeros((1, 1, NCHAN, NBIN)), freqs=FREQS,
+                                              Ps=[0.004], epochs=[(57000, 0, 0.0)], DM=10.0,
+                                              dmc=1))
+    model = archive.load_data("mx_guess", dedisperse=True, tscrunch=True, rm_baseline=True,
+                              quiet=True)
+    try:
+        assert all("_stack" not in archive._registry[nm] for nm in names)
+        assert archive._registry[names[1]].nsub == 1
+        u0, s0, _ = _setup(names, model, False)
+        u1, s1, bulk = _setup(names, model, True)
+        assert bulk is not None and bulk.rows_view is None
+        _same_units(u0, u1)
+        _same_stack(s0, s1)
+    finally:
+        for nm in names + ["mx_guess"]:
+            archive.unregister_archive(nm)
