@@ -31,6 +31,7 @@ import json
 import math
 import os
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -246,9 +247,10 @@ def synth_inputs(eng, config, nsub, seed, sub0):
 # legs beside value: get_TOAs end to end, align_archives at config 5
 # ---------------------------------------------------------------------------
 def leg_get_toas(eng, w, data, reps=3, host=False):
-    """GetTOAs(...).get_TOAs() + the .tim text of every TOA on a registered
-    archive holding the bench's own subints (device tensor, or host numpy for
-    the PCIe-inclusive variant)."""
+    """GetTOAs(...).get_TOAs() + write_TOAs(gt.TOA_list, outfile=...) (the
+    reference's own use, examples/example.py:140) on a registered archive
+    holding the bench's own subints (device tensor, or host numpy for the
+    PCIe-inclusive variant)."""
     import torch
     from pulseportraiture_amd import archive, pplib, pptoas, synth
     from pulseportraiture_amd.mjd import MJD
@@ -260,20 +262,24 @@ def leg_get_toas(eng, w, data, reps=3, host=False):
         telescope_code="gb", backend="bench", frontend="synth",
         epochs=[MJD(57000, int(30 * k), 0.0) for k in range(nsub)]))
     times = []
-    lines = gt = None
+    gt = None
+    tim = os.path.join(tempfile.gettempdir(), "bench_get_toas_%d.tim" % os.getpid())
     for r in range(reps + 1):  # the first call is the warm-up
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         gt = pptoas.GetTOAs([name], synth.EXAMPLE_GMODEL, quiet=True)
         gt.get_TOAs(quiet=True)
-        lines = [pplib.toa_line(t) for t in gt.TOA_list]
+        pplib.write_TOAs(gt.TOA_list, SNR_cutoff=0.0, outfile=tim, append=False)  # example.py:140
         t1 = time.perf_counter()
         if r:
             times.append(t1 - t0)
     archive.unregister_archive(name)
+    with open(tim) as f:
+        nlines = sum(1 for _ in f)
+    os.unlink(tim)
     t = float(np.median(times))
     out = {"value": round(nsub / t, 1), "unit": "TOAs/s", "ms_per_call": round(t * 1e3, 2),
-           "calls": reps, "tim_lines": len(lines),
+           "calls": reps, "tim_lines": nlines,
            "input": "host numpy, streamed through pinned buffers (PCIe-inclusive)" if host
            else "device tensor (HBM-resident)"}
     return out, gt

@@ -14,6 +14,14 @@
 #include "ppfit.h"
 #include "ppfit_kernels.hpp"
 
+// Source hash of this build (pulseportraiture_amd/build.py compares it with
+// today's sources before reusing a built library).
+#ifndef PPF_SRC_HASH
+#define PPF_SRC_HASH "unbuilt"
+#endif
+extern "C" __attribute__((visibility("default"), used)) const char ppf_build_tag[] =
+    "PPF_SRC_HASH=" PPF_SRC_HASH;
+
 using namespace ppf;
 
 namespace {

@@ -22,6 +22,14 @@
 #include <string>
 #include <vector>
 
+// Source hash of this build (pulseportraiture_amd/build.py compares it with
+// today's sources before reusing a built library).
+#ifndef PPF_SRC_HASH
+#define PPF_SRC_HASH "unbuilt"
+#endif
+extern "C" __attribute__((visibility("default"), used)) const char ppfits_build_tag[] =
+    "PPF_SRC_HASH=" PPF_SRC_HASH;
+
 namespace {
 
 constexpr size_t kBlock = 2880;

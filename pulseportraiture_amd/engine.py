@@ -3,6 +3,7 @@
 torch is used only as plumbing: device allocations, H2D/D2H copies and the
 HIP stream handle.  All numerics run in the HIP kernels of libppfit.so.
 """
+import collections
 import ctypes
 
 import numpy as np
@@ -72,6 +73,136 @@ def _bcast(x, n, width, dev, fill=_NAN):
     if t.numel() in (1, width):
         return t.reshape(1, -1).expand(n, width).contiguous()
     raise PPFitError("cannot broadcast %s to (%d, %d)" % (tuple(t.shape), n, width))
+
+
+def _bcast_dev(t, n, width, dev, fill=_NAN):
+    """_bcast for an input already on the device (None: fill)."""
+    if t is None:
+        return torch.full((n, width), fill, dtype=torch.float64, device=dev)
+    if t.numel() == n * width:
+        return t.reshape(n, width).contiguous()
+    if t.numel() in (1, width):
+        return t.reshape(1, -1).expand(n, width).contiguous()
+    raise PPFitError("cannot broadcast %s to (%d, %d)" % (tuple(t.shape), n, width))
+
+
+class _Stager:
+    """The host (numpy) inputs of one call packed into one pinned buffer and
+    copied to the device with one asynchronous H2D on the context stream, so
+    the launches that follow on that stream see them; device tensors pass
+    through unchanged.  add -> a token, run(), then get(token) -> tensor."""
+    _ALIGN = 256
+
+    def __init__(self, dev, stream):
+        self.dev, self.stream = dev, stream
+        self.host, self.nbytes = [], 0
+        self.views = None
+
+    def _add(self, a):
+        if a is None or isinstance(a, torch.Tensor):
+            return ("t", a)
+        a = np.ascontiguousarray(a)
+        off = self.nbytes
+        self.host.append((off, a))
+        self.nbytes = off + (a.nbytes + self._ALIGN - 1) // self._ALIGN * self._ALIGN
+        return ("h", len(self.host) - 1)
+
+    def f64(self, x):
+        if isinstance(x, torch.Tensor):
+            return ("t", x.to(device=self.dev, dtype=torch.float64))
+        return self._add(None if x is None else np.asarray(x, dtype=np.float64))
+
+    def rows(self, x):  # per-subint rows that may hold None (reference defaults)
+        if isinstance(x, torch.Tensor):
+            return ("t", x.to(device=self.dev, dtype=torch.float64))
+        return self._add(None if x is None else _nan_none(x))
+
+    def u8(self, x):
+        if isinstance(x, torch.Tensor):
+            return ("t", x.to(device=self.dev, dtype=torch.uint8))
+        return self._add(None if x is None else np.asarray(x, dtype=np.uint8))
+
+    def i32(self, x):
+        if isinstance(x, torch.Tensor):
+            return ("t", x.to(device=self.dev, dtype=torch.int32).contiguous())
+        return self._add(None if x is None else np.asarray(x, dtype=np.int32))
+
+    def run(self):
+        self.views = []
+        if not self.host:
+            return
+        pin = torch.empty(self.nbytes, dtype=torch.uint8, pin_memory=True)
+        pv = pin.numpy()
+        for off, a in self.host:
+            pv[off:off + a.nbytes] = a.reshape(-1).view(np.uint8)
+        buf = torch.empty(self.nbytes, dtype=torch.uint8, device=self.dev)
+        with torch.cuda.stream(self.stream):
+            buf.copy_(pin, non_blocking=True)
+        self.buf = buf
+        for off, a in self.host:
+            v = buf[off:off + a.nbytes].view(_TORCH_DT[a.dtype.str]).reshape(a.shape)
+            self.views.append(v)
+
+    def get(self, tok):
+        kind, v = tok
+        if kind == "t":
+            return None if v is None else v.contiguous()
+        return self.views[v]
+
+
+_TORCH_DT = {"<f8": torch.float64, "|u1": torch.uint8, "<i4": torch.int32}
+
+# fit results: float64 keys and their widths per subint ("c" = nchan), in
+# the order of one packed device buffer -- the keys the drivers read first,
+# so their host copy is one contiguous prefix (fit_portraits_batch)
+RESULT_F64 = [("params", (5,)), ("param_errs", (5,)), ("nu_out", (3,)), ("cov", (5, 5)),
+              ("scales", "c"), ("scale_errs", "c"), ("channel_snrs", "c"), ("chi2", ()),
+              ("red_chi2", ()), ("snr", ()), ("init_used", (5,)), ("fun", ()),
+              ("cov_nosc", (5, 5)), ("grad", (5,)), ("hess", (5, 5)), ("errs", "c")]
+
+
+def _result_tensors(nsub, nchan, dev):
+    """Result tensors of one fit call as views of one float64 buffer (and
+    nfev / status of one int32 buffer); "_packed" holds (buffer, int32
+    buffer, layout)."""
+    shapes = [(k, (nsub, nchan) if w == "c" else (nsub,) + w) for k, w in RESULT_F64]
+    sizes = [int(np.prod(sh)) for _, sh in shapes]
+    flat = torch.empty(sum(sizes), dtype=torch.float64, device=dev)
+    iflat = torch.empty(2 * nsub, dtype=torch.int32, device=dev)
+    out, lay, o = {}, [], 0
+    for (k, sh), n in zip(shapes, sizes):
+        out[k] = flat[o:o + n].view(sh)
+        lay.append((k, o, sh))
+        o += n
+    out["nfev"], out["status"] = iflat[:nsub], iflat[nsub:]
+    out["_packed"] = (flat, iflat, lay)  # not a tensor: key loops over tensors skip it
+    return out
+
+
+def results_to_host(out, keys=None, stream=None):
+    """Host numpy copies of a fit call's results (keys None: all): one D2H
+    of the packed buffer's span holding them, on the context stream (a copy
+    into pageable memory waits for it).  Results without the packed layout
+    (the streamed path) are copied key by key."""
+    if "_packed" not in out:
+        return {k: v.cpu().numpy() for k, v in out.items()
+                if not k.startswith("_") and (keys is None or k in keys)}
+    flat, iflat, layout = out["_packed"]
+    lay = [(k, o, sh) for k, o, sh in layout if keys is None or k in keys]
+    lo = min((o for _, o, _ in lay), default=0)
+    hi = max((o + int(np.prod(sh)) for _, o, sh in lay), default=0)
+    h = np.empty(max(hi - lo, 0))
+    hi32 = np.empty(iflat.numel(), dtype=np.int32)
+    with torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream()):
+        if hi > lo:
+            torch.from_numpy(h).copy_(flat[lo:hi])
+        torch.from_numpy(hi32).copy_(iflat)
+    res = {k: h[o - lo:o - lo + int(np.prod(sh))].reshape(sh) for k, o, sh in lay}
+    n = len(hi32) // 2
+    for k, a in (("nfev", hi32[:n]), ("status", hi32[n:])):
+        if keys is None or k in keys:
+            res[k] = a
+    return res
 
 
 class Engine:
@@ -204,23 +335,36 @@ class Engine:
         if d.dim() == 2:
             d = d.unsqueeze(0)
         nsub, nchan, nbin = d.shape
-        m = _dev_f64(model, dev)
+        # every host-side (numpy) input goes to the device in one pinned H2D
+        # copy on the context stream; device tensors are used as they are
+        st = _Stager(dev, self.stream)
+        m = st.f64(model)
+        fr = st.f64(freqs)
+        Pt = st.f64(P)
+        it, nf, no = st.rows(init), st.rows(nu_fit), st.rows(nu_out)
+        er = st.f64(errs)
+        mk = st.u8(chan_mask)
+        wt = st.f64(weights)
+        mi = st.i32(model_idx)
+        gn, gt = st.rows(guess_nu), st.rows(guess_tau)
+        st.run()
+        m, fr, Pt, it, nf, no, er, mk, wt, mi, gn, gt = [
+            st.get(x) for x in (m, fr, Pt, it, nf, no, er, mk, wt, mi, gn, gt)]
         if m.dim() == 2:
             m = m.unsqueeze(0)
         if m.shape[1:] != (nchan, nbin):
             raise PPFitError("model shape %s != (nmodel, %d, %d)" % (tuple(m.shape), nchan, nbin))
-        fr = _dev_f64(freqs, dev)
-        fr = fr.expand(nsub, nchan).contiguous() if fr.dim() == 1 else fr.reshape(nsub, nchan)
-        Pt = _dev_f64(P, dev).reshape(-1).expand(nsub).contiguous()
-        it = _bcast(init, nsub, 5, dev)
-        nf = _bcast(nu_fit, nsub, 3, dev)
-        no = _bcast(nu_out, nsub, 3, dev)
-        er = None if errs is None else _dev_f64(errs, dev).reshape(-1, nchan).expand(nsub, nchan).contiguous()
-        mk = None if chan_mask is None else _dev_u8(np.broadcast_to(np.asarray(chan_mask), (nsub, nchan)) if not isinstance(chan_mask, torch.Tensor) else chan_mask.expand(nsub, nchan), dev)
-        wt = None if weights is None else _dev_f64(weights, dev).reshape(-1, nchan).expand(nsub, nchan).contiguous()
-        mi = None if model_idx is None else _dev_i32(model_idx, dev)
-        gn = None if guess_nu is None else _bcast(guess_nu, nsub, 1, dev).reshape(nsub).contiguous()
-        gt = None if guess_tau is None else _bcast(guess_tau, nsub, 1, dev, 0.0).reshape(nsub).contiguous()
+        fr = fr.reshape(-1, nchan).expand(nsub, nchan).contiguous()
+        Pt = Pt.reshape(-1).expand(nsub).contiguous()
+        it = _bcast_dev(it, nsub, 5, dev)
+        nf = _bcast_dev(nf, nsub, 3, dev)
+        no = _bcast_dev(no, nsub, 3, dev)
+        er = None if er is None else er.reshape(-1, nchan).expand(nsub, nchan).contiguous()
+        mk = None if mk is None else mk.reshape(-1, nchan).expand(nsub, nchan).contiguous()
+        wt = None if wt is None else wt.reshape(-1, nchan).expand(nsub, nchan).contiguous()
+        gn = None if guess_nu is None else _bcast_dev(gn, nsub, 1, dev).reshape(nsub).contiguous()
+        gt = None if guess_tau is None else \
+            _bcast_dev(gt, nsub, 1, dev, 0.0).reshape(nsub).contiguous()
         desc = _lib.FitDesc()
         desc.nsub, desc.nchan, desc.nbin, desc.nmodel = nsub, nchan, nbin, m.shape[0]
         for i in range(5):
@@ -241,30 +385,13 @@ class Engine:
                 np.nan if v is None else float(v) for b in bounds for v in (list(b) + [None, None])[:2]])
         desc.bounds = ctypes.cast(bnd, ctypes.c_void_p) if bnd is not None else None
         keep = dict(d=d, m=m, fr=fr, P=Pt, it=it, nf=nf, no=no, er=er, mk=mk, wt=wt,
-                    mi=mi, gn=gn, gt=gt)
+                    mi=mi, gn=gn, gt=gt, staged=getattr(st, "buf", None))
         desc.data, desc.model, desc.model_idx = _ptr(d), _ptr(m), _ptr(mi)
         desc.freqs, desc.errs, desc.chan_mask = _ptr(fr), _ptr(er), _ptr(mk)
         desc.weights, desc.P, desc.init = _ptr(wt), _ptr(Pt), _ptr(it)
         desc.nu_fit, desc.nu_out = _ptr(nf), _ptr(no)
         desc.guess_nu, desc.guess_tau = _ptr(gn), _ptr(gt)
-        f64 = dict(dtype=torch.float64, device=dev)
-        out = dict(params=torch.empty(nsub, 5, **f64),
-                   param_errs=torch.empty(nsub, 5, **f64),
-                   nu_out=torch.empty(nsub, 3, **f64),
-                   cov=torch.empty(nsub, 5, 5, **f64),
-                   scales=torch.empty(nsub, nchan, **f64),
-                   scale_errs=torch.empty(nsub, nchan, **f64),
-                   channel_snrs=torch.empty(nsub, nchan, **f64),
-                   chi2=torch.empty(nsub, **f64), red_chi2=torch.empty(nsub, **f64),
-                   snr=torch.empty(nsub, **f64),
-                   nfev=torch.empty(nsub, dtype=torch.int32, device=dev),
-                   status=torch.empty(nsub, dtype=torch.int32, device=dev),
-                   init_used=torch.empty(nsub, 5, **f64),
-                   fun=torch.empty(nsub, **f64),
-                   cov_nosc=torch.empty(nsub, 5, 5, **f64),
-                   grad=torch.empty(nsub, 5, **f64),
-                   hess=torch.empty(nsub, 5, 5, **f64),
-                   errs=torch.empty(nsub, nchan, **f64))
+        out = _result_tensors(nsub, nchan, dev)
         res = _lib.FitResult()
         for k in ["params", "param_errs", "nu_out", "cov", "scales", "scale_errs",
                   "channel_snrs", "chi2", "red_chi2", "snr", "nfev", "status",
@@ -356,7 +483,7 @@ class Engine:
             free[i % 2].record(comp)
             outs.append(r)
         return {k: torch.cat([o[k] for o in outs]) for k in outs[0]
-                if isinstance(outs[0][k], torch.Tensor)}
+                if isinstance(outs[0][k], torch.Tensor) and not k.startswith("_")}
 
     def phase_shift_batch(self, data, model, noise=None, Ns=100, bounds=(-0.5, 0.5),
                           model_idx=None):
@@ -624,6 +751,118 @@ class Engine:
 
 
 _engines = {}
+
+
+class _PendingHost:
+    """Results of one fit call on their way to the host.  An event marks
+    the end of the call on the context stream; wait() copies the needed
+    span of the packed result buffer into fresh host memory on a side
+    stream that waits for that event only, so later calls queued behind it
+    keep running while the caller reads these results."""
+
+    def __init__(self, out, keys, stream, side):
+        self.flat, self.iflat, layout = out["_packed"]
+        self.lay = [(k, o, sh) for k, o, sh in layout if keys is None or k in keys]
+        self.keys, self.side = keys, side
+        self.event = torch.cuda.Event()
+        self.event.record(stream)
+
+    def wait(self):
+        lo = min((o for _, o, _ in self.lay), default=0)
+        hi = max((o + int(np.prod(sh)) for _, o, sh in self.lay), default=0)
+        h = np.empty(max(hi - lo, 0))
+        hi32 = np.empty(self.iflat.numel(), dtype=np.int32)
+        with torch.cuda.stream(self.side):
+            self.side.wait_event(self.event)
+            if hi > lo:
+                torch.from_numpy(h).copy_(self.flat[lo:hi])
+            torch.from_numpy(hi32).copy_(self.iflat)
+        self.side.synchronize()
+        res = {k: h[o - lo:o - lo + int(np.prod(sh))].reshape(sh) for k, o, sh in self.lay}
+        n = len(hi32) // 2
+        for k, a in (("nfev", hi32[:n]), ("status", hi32[n:])):
+            if self.keys is None or k in self.keys:
+                res[k] = a
+        return res
+
+
+class FitPipeline:
+    """Batched fits submitted one piece at a time, run in submission order on
+    the context stream, with each piece's results collected while later
+    pieces still run -- so the caller's host work on piece i (get_TOAs' TOA
+    records and .tim text) overlaps the device work of pieces i+1, ...
+
+    Host-resident pieces (numpy or CPU tensors) are staged through two
+    pinned buffers and copied to two device buffers on a second stream, the
+    copy of piece i+1 overlapping the fit of piece i (as fit_batch_streamed).
+    submit(tag, data, model, ...) takes fit_batch's arguments; collect()
+    returns (tag, results as host numpy) in submission order."""
+
+    def __init__(self, eng, keys=None):
+        self.eng, self.keys = eng, keys
+        self.pending = collections.deque()
+        self.copy = self.side = None
+        self.slots = [None, None]  # (pinned, device buffer, h2d event, free event)
+        self.k = 0
+
+    def __len__(self):
+        return len(self.pending)
+
+    def _stage(self, host):
+        """Host piece -> device tensor, through slot k % 2."""
+        eng = self.eng
+        hd = host if isinstance(host, torch.Tensor) else torch.from_numpy(
+            np.ascontiguousarray(host, dtype=np.float64))
+        hd = hd.to(torch.float64)
+        n = hd.numel()
+        i = self.k % 2
+        self.k += 1
+        if self.copy is None:
+            self.copy = torch.cuda.Stream(eng.device)
+        slot = self.slots[i]
+        if slot is None or slot[1].numel() < n:
+            if slot is not None:  # in-flight users of the old buffers first
+                for ev in slot[2:]:
+                    if ev is not None:
+                        ev.synchronize()
+            slot = [None, torch.empty(n, dtype=torch.float64, device=eng.device), None, None]
+            self.slots[i] = slot
+        if hd.is_pinned():
+            src = hd.reshape(-1)
+        else:
+            if slot[2] is not None:
+                slot[2].synchronize()  # the pinned buffer's previous H2D is done
+            if slot[0] is None or slot[0].numel() < n:
+                slot[0] = torch.empty(n, dtype=torch.float64, pin_memory=True)
+            slot[0][:n].copy_(hd.reshape(-1))
+            src = slot[0][:n]
+        dbuf, free = slot[1], slot[3]
+        with torch.cuda.stream(self.copy):
+            if free is not None:
+                self.copy.wait_event(free)  # the fit that read the device buffer is done
+            dbuf[:n].copy_(src, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.copy)
+        slot[2] = ev
+        eng.stream.wait_event(ev)
+        return dbuf[:n].view(hd.shape), i
+
+    def submit(self, tag, data, model, freqs, P, init, fit_flags, **kw):
+        slot = None
+        if not isinstance(data, torch.Tensor) or data.device.type == "cpu":
+            data, slot = self._stage(data)
+        out = self.eng.fit_batch(data, model, freqs, P, init, fit_flags, **kw)
+        if slot is not None:
+            ev = torch.cuda.Event()
+            ev.record(self.eng.stream)
+            self.slots[slot][3] = ev
+        if self.side is None:
+            self.side = torch.cuda.Stream(self.eng.device)
+        self.pending.append((tag, out, _PendingHost(out, self.keys, self.eng.stream, self.side)))
+
+    def collect(self):
+        tag, out, ph = self.pending.popleft()
+        return tag, ph.wait()
 
 
 def get_engine(device=None):

@@ -80,10 +80,10 @@ def _settle_arrays(d, s, f):
     return d + iday, s - iday * 86400, f
 
 
-def add_days(epochs_parts, x):
+def add_days_parts(epochs_parts, x):
     """epochs[i] + MJD(x[i]) for float day offsets x, as MJD(x) then __add__
-    compute them (every step elementwise with the same rounding), returned as
-    a list of MJDs."""
+    compute them (every step elementwise with the same rounding), as
+    (days, secs, fracsec) arrays."""
     d0, s0, f0 = epochs_parts
     x = np.asarray(x, dtype=np.float64)
     d = np.trunc(x).astype(np.int64)         # int(dd)
@@ -91,6 +91,11 @@ def add_days(epochs_parts, x):
     s = np.trunc(fd * 86400.0).astype(np.int64)  # int(fd * 86400.0)
     f = fd * 86400.0 - s
     d, s, f = _settle_arrays(d, s, f)
-    d, s, f = _settle_arrays(d0 + d, s0 + s, f0 + f)
+    return _settle_arrays(d0 + d, s0 + s, f0 + f)
+
+
+def add_days(epochs_parts, x):
+    """add_days_parts as a list of MJDs."""
+    d, s, f = add_days_parts(epochs_parts, x)
     mk = MJD._settled
     return [mk(a, b, c) for a, b, c in zip(d.tolist(), s.tolist(), f.tolist())]

@@ -508,7 +508,10 @@ def _flag_fmt(flag, vtype):
     f = flag.replace("%", "%%")
     if hasattr(vtype, "lower"):
         return " -%s %%s" % f
-    if issubclass(vtype, (int, np.integer)) and not issubclass(vtype, (bool, np.bool_)):
+    # Python-2 ints -- bool included (True.bit_length() exists, so
+    # pptoas.py:1602's DM_mean=True prints "1") -- take %d; numpy's bool_ has
+    # no bit_length and takes the float formats
+    if issubclass(vtype, (int, np.integer)) and not issubclass(vtype, np.bool_):
         return " -%s %%d" % f
     if flag.find("_cov") >= 0:
         return " -%s %%.1e" % f
@@ -555,7 +558,21 @@ def toa_line(toa, inf_is_zero=True):
 
 
 def write_TOAs(TOAs, inf_is_zero=True, SNR_cutoff=0.0, outfile=None, append=True):
-    """pplib.py:3451-3509."""
+    """pplib.py:3451-3509.  A get_TOAs TOA_list (toas.TOAList) is written
+    through its column blocks (native .tim writer, include/pptim.h, straight
+    from its buffers to the file); any other sequence of TOAs one line at a
+    time.  Returns None, as the reference does."""
+    from .toas import TOAList, write_pieces
+    if isinstance(TOAs, TOAList):
+        pieces = TOAs.tim_chunks(inf_is_zero, SNR_cutoff)
+        if outfile is None:
+            sys.stdout.flush()
+            write_pieces(sys.stdout.buffer, pieces)
+            sys.stdout.buffer.flush()
+        else:
+            with open(outfile, "ab" if append else "wb") as f:
+                write_pieces(f, pieces)
+        return None
     toas = TOAs if hasattr(TOAs, "__len__") else [TOAs]
     toas = filter_TOAs(toas, "snr", SNR_cutoff, ">=", pass_unflagged=False)
     lines = [toa_line(t, inf_is_zero) for t in toas]
@@ -566,4 +583,3 @@ def write_TOAs(TOAs, inf_is_zero=True, SNR_cutoff=0.0, outfile=None, append=True
         with open(outfile, "a" if append else "w") as f:
             for ln in lines:
                 f.write(ln + "\n")
-    return lines

@@ -7,18 +7,18 @@ and assembles TOA records, Doppler-corrected DMs, flags and the DeltaDM mean
 on the host.  Archives come from ``archive.load_data`` (PSRCHIVE is out of
 scope; see archive.py).
 """
-import gc
 import time
 
 import numpy as np
 
 from . import archive as _arch
-from .mjd import MJD, add_days, epoch_parts
+from .mjd import MJD, add_days_parts, epoch_parts
 from .pplib import (DataBunch, F0_fact, phase_transform, guess_fit_freq, read_model,
                     load_spline_model_file,
                     read_model_device, gen_gaussian_portraits_device, scattering_alpha,
                     weighted_mean, write_TOAs)
-from .pptoaslib import fit_portraits_batch, report_failure
+from .pptoaslib import report_failure
+from .toas import TOA, TOABlock, TOAList, FlagColumn, MJDArray  # noqa: F401
 
 max_nfile = 999
 rm_baseline = bool(F0_fact)  # pptoas.py:25-29
@@ -35,43 +35,19 @@ def _dist_info():
     return 0, 1
 
 
+def fit_pipeline(keys):
+    """The batched-fit pipeline get_TOAs submits its pieces to
+    (engine.FitPipeline on this process's device).  The CPU tests replace it
+    at this boundary with pptoaslib.SyncPipeline over a stand-in fit."""
+    from .engine import FitPipeline, get_engine
+    return FitPipeline(get_engine(), keys=keys)
+
+
 def _shard_range(n, rank, world):
     """Contiguous [lo, hi) of n units for rank; sizes differ by at most one."""
     base, extra = divmod(n, world)
     lo = rank * base + min(rank, extra)
     return lo, lo + base + (1 if rank < extra else 0)
-
-
-class TOA:
-    """TOA record, pptoas.py:31-73.  The reference sets every flag as an
-    attribute (pptoas.py:70-72); here the base fields are slots and a flag
-    attribute reads through to ``flags`` (attributes set later live in the
-    instance dict, which shadows a flag of the same name)."""
-    __slots__ = ("archive", "frequency", "MJD", "TOA_error", "telescope", "telescope_code",
-                 "DM", "DM_error", "flags", "__dict__")
-
-    def __init__(self, archive, frequency, MJD, TOA_error, telescope, telescope_code,
-                 DM=None, DM_error=None, flags={}):
-        self.archive = archive
-        self.frequency = frequency
-        self.MJD = MJD
-        self.TOA_error = TOA_error
-        self.telescope = telescope
-        self.telescope_code = telescope_code
-        self.DM = DM
-        self.DM_error = DM_error
-        self.flags = flags
-
-    def __getattr__(self, name):  # only when no slot / instance attribute has it
-        if name != "flags":
-            try:
-                return self.flags[name]
-            except (KeyError, AttributeError):
-                pass
-        raise AttributeError("'TOA' object has no attribute %r" % name)
-
-    def write_TOA(self, inf_is_zero=True, outfile=None):
-        return write_TOAs(self, inf_is_zero=inf_is_zero, outfile=outfile, append=True)
 
 
 _LIST_ATTRS = ["obs", "doppler_fs", "nu0s", "nu_fits", "nu_refs", "ok_idatafiles", "ok_isubs",
@@ -96,6 +72,12 @@ class GetTOAs:
     most that size (registered in-memory archives are views, read whole)."""
     gather_to = "root"
     read_bytes_max = 8 << 30
+    # device-resident subints of one call are fitted in pieces of these
+    # fractions (at least pipeline_min_subints in all), each piece's TOA
+    # records built while the next runs; pipeline_depth fits in flight
+    pipeline_fracs = (0.45, 0.25, 0.15, 0.1, 0.05)
+    pipeline_min_subints = 2048
+    pipeline_depth = 1
 
     def __init__(self, datafiles, modelfile, quiet=False):
         if isinstance(datafiles, (list, tuple)):
@@ -110,6 +92,7 @@ class GetTOAs:
         self.modelfile = modelfile
         for a in _LIST_ATTRS:
             setattr(self, a, [])
+        self.TOA_list = TOAList()
         self.instrumental_response_dict = self.ird = {"DM": 0.0, "wids": [], "irf_types": []}
         self.quiet = quiet
 
@@ -138,7 +121,7 @@ class GetTOAs:
         return first[order], rank[inv.ravel()]
 
     # -- per-subint templates ------------------------------------------------
-    def _models(self, data, fit_scat, quiet):
+    def _models(self, data, fit_scat, quiet, uniform_freqs=False):
         """Template portrait per ok subint (pptoas.py:351-378), de-duplicated:
         one device build per distinct (channel frequencies, P when TAU is in
         bins of P) key."""
@@ -159,10 +142,13 @@ class GetTOAs:
             self.gparams, self.alpha = gparams, alpha
         tau_P = gparams[1] != 0 and not fit_scat
         ok = np.asarray(data.ok_isubs)
-        keyrows = data.freqs[ok]
-        if tau_P:
-            keyrows = np.concatenate([keyrows, data.Ps[ok][:, None]], axis=1)
-        first, inv = self._row_keys(keyrows)
+        if uniform_freqs and not tau_P:
+            first, inv = np.zeros(1, dtype=np.int64), np.zeros(len(ok), dtype=np.int64)
+        else:
+            keyrows = data.freqs[ok]
+            if tau_P:
+                keyrows = np.concatenate([keyrows, data.Ps[ok][:, None]], axis=1)
+            first, inv = self._row_keys(keyrows)
         idx = np.zeros(nsub, dtype=np.int32)
         idx[ok] = inv
         keyf = data.freqs[ok[first]]
@@ -267,8 +253,14 @@ class GetTOAs:
         shards, one per rank of an initialised torch.distributed group, and a
         rank reads only the subint range of its shard (pptoas.py:246,343 is the
         loop being sharded).  Fits run in one device call per archive and flag
-        set; the per-subint result rows are all-gathered, and every rank
-        assembles the same TOAs in the reference's order."""
+        set.  Every rank turns its own shard's results into columns -- the
+        per-subint arrays and a TOABlock of its TOA records, with the .tim text
+        already formatted when there is more than one rank -- and only those
+        finished columns travel: to rank 0 (``gather_to`` "root", default),
+        which concatenates them in unit order into the per-archive lists and
+        TOA_list, or to every rank ("all").  With "root" the other ranks add
+        nothing to their lists (their shard's blocks stay in
+        ``shard_blocks``)."""
         if quiet is None:
             quiet = self.quiet
         warning = "You are using an experimental functionality of pptoas!"
@@ -290,13 +282,23 @@ class GetTOAs:
         self.add_instrumental_response = add_instrumental_response
         self._fit_flags_prev = None  # the reference's loop-carried fit_flags
         start = time.time()
+        self.phase_s = tm = {}  # wall time per phase of this call (diagnostic)
+        clock = time.perf_counter
+
+        def mark(k, t0):
+            tm[k] = tm.get(k, 0.0) + clock() - t0
+            return clock()
+        t = clock()
         datafiles = self.datafiles if datafile is None else [datafile]
         # 1. metadata of every archive (all ranks; no DATA read)
         jobs = []
+        n_ok0 = len(self.ok_idatafiles)
         for iarch, datafile in enumerate(datafiles):
             try:
+                t = clock()
                 arch = self._open(datafile, tscrunch, quiet)
                 meta = arch.meta
+                t = mark("open", t)
                 if not len(meta.ok_isubs):
                     if not quiet:
                         print("No subints to fit for %s.  Skipping it." % datafile)
@@ -308,55 +310,69 @@ class GetTOAs:
                 continue
             name = datafile if isinstance(datafile, str) else meta.filename
             job = self._prepare(name, meta, nu_refs, nu_fits, fit_scat, method, bounds, quiet)
+            t = mark("prepare", t)
             if job is not None:
                 job.arch = arch
                 jobs.append(job)
-        # 2. shard the units, read and fit this rank's subints
+        # 2. shard the units, read and fit this rank's subints, and turn the
+        # results into columns (arrays + TOA records) on this rank
         rank, world = _dist_info()
         counts = [len(j.ok_isubs) for j in jobs]
         lo, hi = _shard_range(int(sum(counts)), rank, world)
-        parts, durations, off = {}, {}, 0
+        shards, durations, off = {}, {}, 0
+        pipe = None
+        pend = {}  # piece id -> [ij, a0, nsubs, groups left, result arrays]
         for ij, job in enumerate(jobs):
             a0, a1 = max(lo, off) - off, min(hi, off + counts[ij]) - off
             off += counts[ij]
             if a1 <= a0:
                 continue
-            t0 = time.time()
-            parts[ij] = (a0, self._fit_job(job, a0, a1, fit_scat, method))
-            durations[ij] = time.time() - t0
-        # 3. gather the result arrays: to rank 0 (gather_to "root"), which
-        # assembles every TOA, or to every rank ("all")
+            if pipe is None:
+                pipe = fit_pipeline(_RESULT_KEYS)
+            t = clock()
+            pa0 = a0
+            for rsubs in self._read_pieces(job, job.ok_isubs[a0:a1]):
+                s_lo, sub, errs = self._read(job, rsubs, fit_scat)
+                t = mark("read", t)
+                for subs in self._pipe_split(rsubs, sub):
+                    self._submit(pipe, pend, (ij, pa0), job, subs, s_lo, sub, errs, fit_scat,
+                                 method)
+                    pa0 += len(subs)
+                    t = mark("submit", t)
+                    while len(pipe) > self.pipeline_depth:
+                        self._collect(pipe, pend, jobs, shards, durations,
+                                      (print_phase, print_flux, print_parangle,
+                                       addtnl_toa_flags), mark)
+                        t = clock()
+        while pipe is not None and len(pipe):
+            self._collect(pipe, pend, jobs, shards, durations,
+                          (print_phase, print_flux, print_parangle, addtnl_toa_flags), mark)
+        self.shard_blocks = [sh.block for ij in sorted(shards) for sh in shards[ij]]
+        # 3. gather the finished columns: to rank 0 (gather_to "root") or to
+        # every rank ("all")
+        t = clock()
         if world > 1:
             import torch.distributed as dist
             if self.gather_to == "all":
                 got = [None] * world
-                dist.all_gather_object(got, (parts, durations))
+                dist.all_gather_object(got, (shards, durations))
             else:
                 got = [None] * world if rank == 0 else None
-                dist.gather_object((parts, durations), got, dst=0)
-                if rank != 0:
-                    self.ok_idatafiles = []  # the results live on rank 0
+                dist.gather_object((shards, durations), got, dst=0)
+                if rank != 0:  # the results live on rank 0
+                    del self.ok_idatafiles[n_ok0:]
                     return
-            parts, durations = {}, {}
-            for p_r, d_r in got:
-                for ij, v in p_r.items():
-                    parts.setdefault(ij, []).append(v)
+            shards, durations = {}, {}
+            for s_r, d_r in got:
+                for ij, v in s_r.items():
+                    shards.setdefault(ij, []).extend(v)
                 for ij, t in d_r.items():
                     durations[ij] = durations.get(ij, 0.0) + t
-        else:
-            parts = {ij: [v] for ij, v in parts.items()}
-        gc_on = gc.isenabled()
-        gc.disable()  # a few containers per TOA: keep the cyclic collector out of assembly
-        try:
-            for ij, job in enumerate(jobs):
-                pieces = sorted(parts[ij], key=lambda v: v[0])
-                res = pieces[0][1] if len(pieces) == 1 else \
-                    {k: np.concatenate([p[1][k] for p in pieces]) for k in pieces[0][1]}
-                self._assemble(job, res, print_phase, print_flux, print_parangle,
-                               addtnl_toa_flags, durations.get(ij, 0.0), quiet)
-        finally:
-            if gc_on:
-                gc.enable()
+        t = mark("gather", t)
+        for ij, job in enumerate(jobs):
+            self._finish(job, sorted(shards[ij], key=lambda v: v.a0),
+                         durations.get(ij, 0.0), quiet)
+        mark("finish", t)
         tot = time.time() - start
         if not quiet and len(self.ok_isubs):
             n = np.array([len(x) for x in self.ok_isubs]).sum()
@@ -734,7 +750,17 @@ class GetTOAs:
         ep = data.get("epoch_parts") or epoch_parts(data.epochs)
         MJDs = ep[0] + (ep[1] + ep[2]) / 86400.0  # MJD.in_days elementwise
         ok_isubs = np.asarray(data.ok_isubs)
-        mm = self._models(data, fit_scat, quiet)
+        wn = np.asarray(data.weights) != 0.0
+        mask = wn.astype(np.uint8)
+        # per-channel rows every ok subint shares (one row to the device,
+        # one template key, one guess_fit_freq)
+        dense = len(ok_isubs) == nsub
+
+        def okrows(a):
+            return a if dense else a[ok_isubs]
+        uniform = {k: bool(len(ok_isubs)) and bool((okrows(a) == okrows(a)[0]).all())
+                   for k, a in (("freqs", data.freqs), ("mask", mask), ("weights", data.weights))}
+        mm = self._models(data, fit_scat, quiet, uniform["freqs"])
         if mm is None:
             if not quiet:
                 print("Model nbin/nchan mismatch for %s; skipping it." % datafile)
@@ -742,10 +768,12 @@ class GetTOAs:
         models, midx, _ = mm
         if self._irf_active():
             models, midx = self._irf_models(models, midx, data, ok_isubs)
-        wn = np.asarray(data.weights) != 0.0
-        mask = wn.astype(np.uint8)
         nchx = wn.sum(axis=1)
         allok = nchx == nchan
+        # the tobs flag's values: typed when the durations are numbers
+        tobs = np.asarray(data.subtimes)
+        if tobs.dtype.kind not in "fiu":
+            tobs = np.asarray(data.subtimes, dtype=object)
         # reference frequencies (pptoas.py:396-415)
         nu_fits_a = np.zeros((nsub, 3))
         nu_refs_a = np.full((nsub, 3), np.nan)
@@ -758,7 +786,7 @@ class GetTOAs:
         guess_tau = np.zeros(nsub)
         init[ok_isubs, 1] = DM_stored
         self._nu_fit_and_tau(data, ok_isubs, wn, allok, nu_fit_tuple, fit_scat, nu_fits_a, init,
-                             guess_tau)
+                             guess_tau, uniform["freqs"])
         # per-subint fit flags (pptoas.py:474-484): get_TOAs keeps one
         # fit_flags list across subints and archives, and a 2-channel subint
         # (fit_DM and fit_GM) zeroes GM in the *previous* subint's list --
@@ -789,14 +817,14 @@ class GetTOAs:
             bounds = [(None, None), (None, None), (None, None),
                       (np.log10((10 * nbin) ** -1), None) if self.log10_tau else (0.0, None),
                       (-10.0, 10.0)]
-        return DataBunch(name=datafile, data=data, obs=obs, DM0=DM0, MJDs=MJDs, epoch_parts=ep,
-                         ok_isubs=ok_isubs, models=models, midx=midx, mask=mask, wn=wn,
-                         nchx=nchx, nu_fits_a=nu_fits_a, nu_refs_a=nu_refs_a, init=init,
-                         guess_tau=guess_tau, ff=ff_all, bounds=bounds, allok=allok,
-                         nu_fit_tuple=nu_fit_tuple)
+        return _Job(name=datafile, data=data, obs=obs, DM0=DM0, MJDs=MJDs, epoch_parts=ep,
+                    ok_isubs=ok_isubs, models=models, midx=midx, mask=mask, wn=wn,
+                    nchx=nchx, nu_fits_a=nu_fits_a, nu_refs_a=nu_refs_a, init=init,
+                    guess_tau=guess_tau, ff=ff_all, bounds=bounds, allok=allok,
+                    nu_fit_tuple=nu_fit_tuple, uniform=uniform, tobs=tobs)
 
     def _nu_fit_and_tau(self, data, isubs, wn, allok, nu_fit_tuple, fit_scat, nu_fits_a, init,
-                        guess_tau):
+                        guess_tau, uniform_freqs=False):
         """nu_fit (guess_fit_freq with the channel S/Ns, pptoas.py:396-415)
         and the scattering guess at nu_fit_tau (pptoas.py:420-440) of subints
         isubs, into nu_fits_a / init / guess_tau."""
@@ -804,7 +832,8 @@ class GetTOAs:
             return
         nbin = data.nbin
         if nu_fit_tuple is None:
-            nu_fits_a[isubs] = self._guess_fit_freqs(data, isubs, wn, allok)[:, None]
+            nu_fits_a[isubs] = self._guess_fit_freqs(data, isubs, wn, allok,
+                                                     uniform_freqs)[:, None]
         else:
             nu_fits_a[isubs] = [nu_fit_tuple[0], nu_fit_tuple[0], nu_fit_tuple[-1]]
         if fit_scat:
@@ -825,13 +854,17 @@ class GetTOAs:
             init[isubs, 4] = alpha_g
 
     @staticmethod
-    def _guess_fit_freqs(data, ok_isubs, wn, allok):
+    def _guess_fit_freqs(data, ok_isubs, wn, allok, uniform_freqs=False):
         """guess_fit_freq(freqsx, SNRsx) of every ok subint (pptoas.py:401,
-        pplib.py:2618-2632): whole rows at once where every channel is on
-        (numpy's row sums are its 1-D sums), the compressed rows otherwise."""
-        f = data.freqs[ok_isubs]
-        snr = np.asarray(data.SNRs)[ok_isubs, 0]
-        if allok[ok_isubs].all() and (f == f[0]).all() and (snr == snr[0]).all():
+        pplib.py:2618-2632): once when every such subint has the same
+        frequencies, all channels on and the same S/Ns; whole rows at once
+        where every channel is on (numpy's row sums are its 1-D sums), the
+        compressed rows otherwise."""
+        dense = len(ok_isubs) == data.nsub
+        f = data.freqs if dense else data.freqs[ok_isubs]
+        snr = np.asarray(data.SNRs)[:, 0] if dense else np.asarray(data.SNRs)[ok_isubs, 0]
+        alla = bool(allok.all()) if dense else bool(allok[ok_isubs].all())
+        if alla and uniform_freqs and (snr == snr[0]).all():
             return np.full(len(ok_isubs), guess_fit_freq(f[0], snr[0]))  # one distinct row
         nu0 = (f.min(axis=1) + f.max(axis=1)) * 0.5
         f2 = f ** -2
@@ -858,35 +891,49 @@ class GetTOAs:
             i = j
         return out
 
-    def _fit_job(self, job, a0, a1, fit_scat, method):
-        """Fit ok subints job.ok_isubs[a0:a1] of one archive: read only their
-        subint range, in pieces of at most read_bytes_max, then one batched
-        device call per piece and flag set.  Returns result rows aligned with
-        job.ok_isubs[a0:a1]."""
-        pieces = self._read_pieces(job, job.ok_isubs[a0:a1])
-        res = [self._fit_piece(job, p, fit_scat, method) for p in pieces]
-        if len(res) == 1:
-            return res[0]
-        return {k: np.concatenate([r[k] for r in res]) for k in res[0]}
-
-    def _fit_piece(self, job, subs, fit_scat, method):
+    def _read(self, job, subs, fit_scat):
+        """Read the subint range of subs (one read piece): (first subint,
+        [n, nchan, nbin] numpy or device view, noise rows or None).  A
+        PSRFITS archive's deferred SNRs (Profile::snr(), pplib.py:2762-2770)
+        come from the data just read, then those subints' nu_fit and
+        scattering guess."""
         data = job.data
         s_lo, s_hi = int(subs[0]), int(subs[-1]) + 1
         full = job.arch.read(s_lo, s_hi)  # [s_hi - s_lo, npol, nchan, nbin], numpy or device
         if data.get("snr_deferred"):
-            # load_data's SNRs (Profile::snr(), pplib.py:2762-2770) of the
-            # subints just read, then their nu_fit and scattering guess
             from .engine import get_engine
             data.SNRs[s_lo:s_hi] = get_engine().profile_snr(full).cpu().numpy()
             self._nu_fit_and_tau(data, subs, job.wn, job.allok, job.nu_fit_tuple, fit_scat,
-                                 job.nu_fits_a, job.init, job.guess_tau)
-        sub = full[:, 0]
+                                 job.nu_fits_a, job.init, job.guess_tau, job.uniform["freqs"])
         ns = data.get("noise_stds")
-        errs = None if ns is None else np.asarray(ns)[:, 0]
+        return s_lo, full[:, 0], None if ns is None else np.asarray(ns)[:, 0]
+
+    def _pipe_split(self, subs, sub):
+        """Pipeline pieces of one read piece: host-resident subints in pieces
+        of at most STREAM_CHUNK_BYTES (their copies overlap the fits), device-
+        resident ones in shrinking fractions (pipeline_fracs) so that the
+        host work after the last piece is small."""
+        n = len(subs)
+        if _arch._is_tensor(sub) and sub.device.type != "cpu":
+            if n < self.pipeline_min_subints:
+                return [subs]
+            cuts = np.cumsum([0.0] + list(self.pipeline_fracs))
+            cuts = np.unique(np.round(cuts / cuts[-1] * n).astype(int))
+        else:
+            from .pptoaslib import STREAM_CHUNK_BYTES
+            per = 8 * int(np.prod(sub.shape[1:]))
+            step = max(1, STREAM_CHUNK_BYTES // per)
+            cuts = np.unique(np.append(np.arange(0, n, step), n))
+        return [subs[i:j] for i, j in zip(cuts[:-1], cuts[1:]) if j > i]
+
+    def _submit(self, pipe, pend, key, job, subs, s_lo, sub, errs, fit_scat, method):
+        """Launch the fits of subints subs (one device call per fit-flag
+        group) into the pipeline; piece key = (archive index, a0)."""
+        data = job.data
         ffs = job.ff[subs]
         groups = [np.arange(len(subs))] if (ffs == ffs[0]).all() else \
             [np.flatnonzero((ffs == r).all(axis=1)) for r in np.unique(ffs, axis=0)]
-        out = None
+        pend[key] = [len(groups), len(subs), None, time.time()]
         for g in groups:
             s = subs[g]
             rel = s - s_lo
@@ -895,37 +942,61 @@ class GetTOAs:
             else:
                 d = sub[rel] if not _arch._is_tensor(sub) else sub[_arch_index(rel, sub)]
             # errs None: the device estimates get_noise_PS per channel, as
-            # load_data's noise_stds (pplib.py:2744-2748)
-            res = fit_portraits_batch(
-                d, job.models, job.init[s], data.Ps[s], data.freqs[s],
-                nu_fits=job.nu_fits_a[s], nu_outs=job.nu_refs_a[s],
-                errs=None if errs is None else errs[s], fit_flags=list(ffs[g[0]]),
-                log10_tau=self.log10_tau, option=0, is_toa=True,
-                chan_mask=job.mask[s], weights=data.weights[s],
-                model_idx=job.midx[s], guess=True, guess_Ns=100, guess_wrap=True,
-                guess_nu=None, guess_tau=job.guess_tau[s] if fit_scat else None,
-                method=method, bounds=job.bounds)
-            keep = {k: np.asarray(res[k]) for k in _RESULT_KEYS if k in res}
-            keep["nu_fit"] = job.nu_fits_a[s]  # the assembling rank's nu_fits
-            if len(groups) == 1:
-                return keep
-            if out is None:
-                out = {k: np.zeros((len(subs),) + v.shape[1:], dtype=v.dtype)
-                       for k, v in keep.items()}
-            for k, v in keep.items():
-                out[k][g] = v
-        return out
+            # load_data's noise_stds (pplib.py:2744-2748); per-channel rows
+            # shared by every subint go as one row
+            pipe.submit((key, g, _take(job.nu_fits_a, s)),
+                        d, job.models, job.row("freqs", s), _take(data.Ps, s),
+                        _take(job.init, s), list(ffs[g[0]]),
+                        nu_fit=_take(job.nu_fits_a, s), nu_out=_take(job.nu_refs_a, s),
+                        errs=None if errs is None else _take(errs, s),
+                        log10_tau=self.log10_tau, option=0, is_toa=True,
+                        chan_mask=job.row("mask", s), weights=job.row("weights", s),
+                        model_idx=_take(job.midx, s), guess=True, guess_Ns=100,
+                        guess_wrap=True, guess_nu=None,
+                        guess_tau=_take(job.guess_tau, s) if fit_scat else None,
+                        method=method, bounds=job.bounds)
 
-    def _assemble(self, job, res, print_phase, print_flux, print_parangle, addtnl_toa_flags,
-                  fit_duration, quiet):
-        """Host bookkeeping of pptoas.py:522-720 from the device results, as
-        array operations; one TOA record per ok subint."""
+    def _collect(self, pipe, pend, jobs, shards, durations, toa_args, mark):
+        """Collect the oldest fit in the pipeline; when its piece is complete,
+        turn it into columns on this rank (_shard; its .tim text formatted
+        now, while later pieces still run on the device)."""
+        t = time.perf_counter()
+        (key, g, nu_fit), res = pipe.collect()
+        t = mark("wait", t)
+        p = pend[key]
+        keep = {k: res[k] for k in _RESULT_KEYS if k in res}
+        keep["nu_fit"] = nu_fit  # the assembling rank's nu_fits
+        if p[0] == 1 and p[2] is None:
+            out = keep
+        else:
+            if p[2] is None:
+                p[2] = {k: np.zeros((p[1],) + v.shape[1:], dtype=v.dtype) for k, v in keep.items()}
+            for k, v in keep.items():
+                p[2][k][g] = v
+            out = p[2]
+        p[0] -= 1
+        if p[0]:
+            return
+        del pend[key]
+        ij, a0 = key
+        durations[ij] = durations.get(ij, 0.0) + time.time() - p[3]
+        sh = self._shard(jobs[ij], a0, out, *toa_args)
+        t = mark("shard", t)
+        sh.block.preformat()  # the .tim text of these records
+        mark("preformat", t)
+        shards.setdefault(ij, []).append(sh)
+
+    def _shard(self, job, a0, res, print_phase, print_flux, print_parangle, addtnl_toa_flags):
+        """Columns of ok subints job.ok_isubs[a0:a0 + n] from their device
+        results (pptoas.py:522-661), on the rank that fitted them: the
+        per-subint values in ok order and a TOABlock of their TOA records
+        (flags in the reference's insertion order, pptoas.py:606-661, then
+        addtnl_toa_flags)."""
         data, datafile = job.data, job.name
-        nsub, nchan, nbin = data.nsub, data.nchan, data.nbin
-        ok = job.ok_isubs
-        nok = len(ok)
-        z = lambda *s: np.zeros(s, dtype=np.float64)
+        nchan = data.nchan
         p, e = res["params"], res["param_errs"]
+        n = len(p)
+        ok = job.ok_isubs[a0:a0 + n]
         status, nfev = res["status"].astype(np.int64), res["nfev"].astype(np.int64)
         for j in np.flatnonzero(~np.isin(status, (0, 1, 2, 4))):
             report_failure(int(status[j]), "%s_%d" % (datafile, ok[j]))
@@ -933,125 +1004,186 @@ class GetTOAs:
         P = data.Ps[ok]
         phi, phi_err = p[:, 0], e[:, 0]
         DM, DM_err, GM, GM_err = p[:, 1].copy(), e[:, 1], p[:, 2].copy(), e[:, 2]
-        toa_mjds = add_days(tuple(x[ok] for x in job.epoch_parts),
-                            ((phi * P) + data.backend_delay) / (3600 * 24.))
+        mjd = add_days_parts(tuple(x[ok] for x in job.epoch_parts),
+                             ((phi * P) + data.backend_delay) / (3600 * 24.))
         TOA_err = phi_err * P * 1e6
         if self.bary:
             df = np.asarray(data.doppler_factors, dtype=np.float64)[ok]
             DM = np.where(ff[:, 1] != 0, DM * df, DM)
             GM = np.where(ff[:, 2] != 0, GM * df ** 3, GM)
         else:
-            df = np.ones(nok)
-        wn = job.wn[ok]
+            df = np.ones(n)
+        wn = _take(job.wn, ok)
         wall = bool(wn.all())
         sc = res["scales"] if wall else np.where(wn, res["scales"], 0.0)
         sce = res["scale_errs"] if wall else np.where(wn, res["scale_errs"], 0.0)
+        chs = res["channel_snrs"] if wall else np.where(wn, res["channel_snrs"], 0.0)
         nuo = res["nu_out"]
-        phis, phi_errs, DMs, DM_errs = z(nsub), z(nsub), z(nsub), z(nsub)
-        GMs, GM_errs, taus, tau_errs = z(nsub), z(nsub), z(nsub), z(nsub)
-        alphas, alpha_errs, snrs, red_chi2s = z(nsub), z(nsub), z(nsub), z(nsub)
-        fluxes, flux_errs, flux_freqs = z(nsub), z(nsub), z(nsub)
-        scales, scale_errs, chsnrs = z(nsub, nchan), z(nsub, nchan), z(nsub, nchan)
-        pfl, pfle = z(nsub, nchan), z(nsub, nchan)
-        covs = z(nsub, self.nfit, self.nfit)
-        nfevals = np.zeros(nsub, dtype="int")
-        rcs = np.zeros(nsub, dtype="int")
-        TOAs = np.zeros(nsub, dtype="object")
-        TOA_errs = np.zeros(nsub, dtype="object")
-        phis[ok], phi_errs[ok] = phi, phi_err
-        TOAs[ok] = toa_mjds
-        TOA_errs[ok] = TOA_err
-        DMs[ok], DM_errs[ok], GMs[ok], GM_errs[ok] = DM, DM_err, GM, GM_err
-        taus[ok], tau_errs[ok] = p[:, 3], e[:, 3]
-        alphas[ok], alpha_errs[ok] = p[:, 4], e[:, 4]
-        nfevals[ok], rcs[ok] = nfev, status
-        scales[ok], scale_errs[ok] = sc, sce
-        snrs[ok] = res["snr"]
-        chsnrs[ok] = res["channel_snrs"] if wall else np.where(wn, res["channel_snrs"], 0.0)
-        red_chi2s[ok] = res["red_chi2"]
         nf = ff.sum(axis=1)
         cov = res["cov"]
         full = nf == self.nfit
         if full.all():
-            covs[ok] = cov[:, :self.nfit, :self.nfit]
+            covs = np.ascontiguousarray(cov[:, :self.nfit, :self.nfit])
         else:
-            for j in range(nok):
+            covs = np.zeros((n, self.nfit, self.nfit))
+            covs[full] = cov[full][:, :self.nfit, :self.nfit]
+            for j in np.flatnonzero(~full):
                 cm = cov[j][:nf[j], :nf[j]]
                 try:  # the reference's assignment, broadcasting a 1x1 block
-                    covs[ok[j]] = cm
+                    covs[j] = cm
                 except ValueError:
                     w = np.where(ff[j])[0]
                     for ii, ifit in enumerate(w):
                         for jj, jfit in enumerate(w):
-                            covs[ok[j]][ifit, jfit] = cm[ii, jj]
-        fo = data.freqs[ok]
-        fmax = (fo if wall else np.where(wn, fo, -np.inf)).max(axis=1)
-        fmin = (fo if wall else np.where(wn, fo, np.inf)).min(axis=1)
+                            covs[j][ifit, jfit] = cm[ii, jj]
+        if wall and job.uniform["freqs"]:  # every row the same: its extremes
+            f0 = data.freqs[ok[0]]
+            fmax, fmin = np.full(n, f0.max()), np.full(n, f0.min())
+        else:
+            fo = _take(data.freqs, ok)
+            fmax = (fo if wall else np.where(wn, fo, -np.inf)).max(axis=1)
+            fmin = (fo if wall else np.where(wn, fo, np.inf)).min(axis=1)
+        flux = None
         if print_flux:
             # scattering keeps each row's mean, so the scattered model's
             # channel means are the template's (pptoas.py:553-575)
+            pfl, pfle = np.zeros((n, nchan)), np.zeros((n, nchan))
+            fluxes, flux_errs, flux_freqs = np.zeros(n), np.zeros(n), np.zeros(n)
             for j, isub in enumerate(ok):
                 okc = wn[j]
                 means = job.models[job.midx[isub]][okc].mean(axis=1)
-                pfl[isub, okc] = means * sc[j][okc]
-                pfle[isub, okc] = abs(means) * sce[j][okc]
-                fluxes[isub], flux_errs[isub] = weighted_mean(pfl[isub, okc], pfle[isub, okc])
-                flux_freqs[isub] = weighted_mean(data.freqs[isub, okc], pfle[isub, okc])[0]
-        # TOA records: flags in the reference's insertion order (pptoas.py:606-661)
-        has_ref = ~np.isnan(job.nu_refs_a[ok, 0])
-        cols = {}
-        cols["gm"], cols["gm_err"] = GM, GM_err
-        if self.log10_tau:
-            cols["scat_time"] = 10 ** p[:, 3] * P / df * 1e6
-            cols["log10_scat_time"] = p[:, 3] + np.log10(P / df)
-            cols["log10_scat_time_err"] = e[:, 3]
-        else:
-            cols["scat_time"] = p[:, 3] * P / df * 1e6
-            cols["scat_time_err"] = e[:, 3] * P / df * 1e6
-        cols["scat_ref_freq"] = nuo[:, 2] * df
-        cols["scat_ind"] = p[:, 4]
-        cols["scat_ind_err"] = e[:, 4]
-        subt = np.asarray(data.subtimes, dtype=object)[ok]
-        common = [("be", [data.backend] * nok), ("fe", [data.frontend] * nok),
-                  ("f", [data.frontend + "_" + data.backend] * nok), ("nbin", [nbin] * nok),
-                  ("nch", [nchan] * nok), ("nchx", job.nchx[ok].tolist()),
-                  ("bw", (fmax - fmin).tolist()), ("chbw", [abs(data.bw) / nchan] * nok),
-                  ("subint", ok.tolist()), ("tobs", subt.tolist()),
-                  ("fratio", (fmax / fmin).tolist()), ("tmplt", [self.modelfile] * nok),
-                  ("snr", res["snr"].tolist())]
-        cov01 = cov[:, 0, 1].tolist()
-        gof = res["red_chi2"].tolist()
-        tail = []
+                pfl[j, okc] = means * sc[j][okc]
+                pfle[j, okc] = abs(means) * sce[j][okc]
+                fluxes[j], flux_errs[j] = weighted_mean(pfl[j, okc], pfle[j, okc])
+                flux_freqs[j] = weighted_mean(data.freqs[isub, okc], pfle[j, okc])[0]
+            flux = (pfl, pfle, fluxes, flux_errs, flux_freqs)
+        # TOA records as columns; a flag some rows lack carries a presence mask
+        cols = []
+
+        def col(key, vals, present=None):
+            if present is not None:
+                if not present.any():
+                    return
+                if present.all():
+                    present = None
+            cols.append(FlagColumn.of(key, vals, n, present))
+
+        gp = ff[:, 2] != 0
+        if gp.any():
+            col("gm", GM, gp)
+            col("gm_err", GM_err, gp)
+        tp = ff[:, 3] != 0
+        if tp.any():
+            if self.log10_tau:
+                col("scat_time", 10 ** p[:, 3] * P / df * 1e6, tp)
+                col("log10_scat_time", p[:, 3] + np.log10(P / df), tp)
+                col("log10_scat_time_err", e[:, 3], tp)
+            else:
+                col("scat_time", p[:, 3] * P / df * 1e6, tp)
+                col("scat_time_err", e[:, 3] * P / df * 1e6, tp)
+            col("scat_ref_freq", nuo[:, 2] * df, tp)
+            col("scat_ind", p[:, 4], tp)
+        col("scat_ind_err", e[:, 4], ff[:, 4] != 0)
+        const = FlagColumn
+        cols += [const("be", "const", data.backend), const("fe", "const", data.frontend),
+                 const("f", "const", data.frontend + "_" + data.backend),
+                 const("nbin", "const", data.nbin), const("nch", "const", nchan)]
+        col("nchx", job.nchx[ok])
+        col("bw", fmax - fmin)
+        cols.append(const("chbw", "const", abs(data.bw) / nchan))
+        col("subint", ok)
+        col("tobs", _take(job.tobs, ok))
+        col("fratio", fmax / fmin)
+        cols.append(const("tmplt", "const", self.modelfile))
+        col("snr", res["snr"])
+        col("phi_DM_cov", cov[:, 0, 1],
+            ~np.isnan(job.nu_refs_a[ok, 0]) & (ff[:, 0] != 0) & (ff[:, 1] != 0))
+        col("gof", res["red_chi2"])
         if print_phase:
-            tail += [("phs", phi.tolist()), ("phs_err", phi_err.tolist())]
+            col("phs", phi)
+            col("phs_err", phi_err)
         if print_flux:
-            tail += [("flux", fluxes[ok].tolist()), ("flux_err", flux_errs[ok].tolist()),
-                     ("flux_ref_freq", flux_freqs[ok].tolist())]
+            col("flux", flux[2])
+            col("flux_err", flux[3])
+            col("flux_ref_freq", flux[4])
         if print_parangle:
-            tail += [("par_angle", np.asarray(data.parallactic_angles)[ok].tolist())]
-        extra = list(addtnl_toa_flags.items())
-        # one key list per (fit flags, phi_DM_cov present) pattern
-        pat = ff * np.array([1, 2, 4, 8, 16])
-        pat = pat.sum(axis=1) * 2 + (has_ref & (ff[:, 0] != 0) & (ff[:, 1] != 0))
-        used = set()
-        if ff[:, 2].any():
-            used |= {"gm", "gm_err"}
-        if ff[:, 3].any():
-            used |= {"scat_time", "log10_scat_time", "log10_scat_time_err", "scat_time_err",
-                     "scat_ref_freq", "scat_ind"}
-        if ff[:, 4].any():
-            used.add("scat_ind_err")
-        colv = {k: np.asarray(v).tolist() for k, v in cols.items() if k in used}
-        toas = [None] * nok
-        self._make_toas(toas, pat, ff, colv, common, cov01, gof, tail, extra, datafile,
-                        data.telescope, data.telescope_code, nuo[:, 0].tolist(),
-                        toa_mjds, TOA_err.tolist(), DM.tolist(), DM_err.tolist())
-        self.TOA_list.extend(toas)
-        job.nu_fits_a[ok] = res["nu_fit"]  # (computed by whichever rank read the subint)
-        nu_fits = list(job.nu_fits_a)  # list(np.zeros([nsub, 3])) filled (pptoas.py:283,406)
-        nr = np.zeros((nsub, 3))  # pptoas.py:284, ok rows from the fit (:527-530)
-        nr[ok] = nuo
-        nu_refs = nr.tolist()
+            col("par_angle", np.asarray(data.parallactic_angles)[ok])
+        dp = ff[:, 1] != 0
+        block = TOABlock(datafile, data.telescope, data.telescope_code, nuo[:, 0], mjd, TOA_err,
+                         dm=DM if dp.any() else None, dme=DM_err if dp.any() else None,
+                         dm_present=None if dp.all() else dp, cols=cols)
+        block.add_flags(list(addtnl_toa_flags.items()))
+        return DataBunch(a0=a0, n=n, phi=phi, phi_err=phi_err, DM=DM, DM_err=DM_err, GM=GM,
+                         GM_err=GM_err, tau=p[:, 3], tau_err=e[:, 3], alpha=p[:, 4],
+                         alpha_err=e[:, 4], nfev=nfev, status=status, scales=sc, scale_errs=sce,
+                         chsnrs=chs, snr=res["snr"], red_chi2=res["red_chi2"], covs=covs,
+                         nu_out=nuo, nu_fit=res["nu_fit"], mjd=mjd, TOA_err=TOA_err, flux=flux,
+                         block=block)
+
+    def _finish(self, job, shards, fit_duration, quiet):
+        """The per-archive lists of pptoas.py:662-720 (and the DeltaDM mean,
+        :664-681) from the shards' columns, concatenated in unit order; the
+        shards' TOABlocks join TOA_list."""
+        data, datafile = job.data, job.name
+        nsub, nchan = data.nsub, data.nchan
+        ok = job.ok_isubs
+        nok = len(ok)
+        if len(shards) == 1:
+            def cat(k):
+                return shards[0][k]
+        else:
+            def cat(k):
+                return np.concatenate([sh[k] for sh in shards])
+        dense = nok == nsub  # ok_isubs is then every subint, in order
+
+        def spread(v, tail=(), dtype=np.float64):
+            if dense:
+                return np.ascontiguousarray(v, dtype=dtype)
+            out = np.zeros((nsub,) + tail, dtype=dtype)
+            out[ok] = v
+            return out
+
+        phis, phi_errs = spread(cat("phi")), spread(cat("phi_err"))
+        DMs, DM_errs = spread(cat("DM")), spread(cat("DM_err"))
+        GMs, GM_errs = spread(cat("GM")), spread(cat("GM_err"))
+        taus, tau_errs = spread(cat("tau")), spread(cat("tau_err"))
+        alphas, alpha_errs = spread(cat("alpha")), spread(cat("alpha_err"))
+        nfevals, rcs = spread(cat("nfev"), dtype="int"), spread(cat("status"), dtype="int")
+        scales = spread(cat("scales"), (nchan,))
+        scale_errs = spread(cat("scale_errs"), (nchan,))
+        chsnrs = spread(cat("chsnrs"), (nchan,))
+        snrs, red_chi2s = spread(cat("snr")), spread(cat("red_chi2"))
+        covs = spread(cat("covs"), (self.nfit, self.nfit))
+        if shards[0].flux is not None:
+            fl = [np.concatenate([sh.flux[i] for sh in shards]) for i in range(5)]
+            pfl, pfle = spread(fl[0], (nchan,)), spread(fl[1], (nchan,))
+            fluxes, flux_errs, flux_freqs = spread(fl[2]), spread(fl[3]), spread(fl[4])
+        else:
+            pfl, pfle = np.zeros((nsub, nchan)), np.zeros((nsub, nchan))
+            fluxes, flux_errs, flux_freqs = np.zeros(nsub), np.zeros(nsub), np.zeros(nsub)
+        mjd = [np.concatenate([sh.mjd[i] for sh in shards]) for i in range(3)]
+        if dense:
+            TOAs = MJDArray(*mjd)
+        else:
+            parts = []
+            for i, dt in enumerate((np.int64, np.int64, np.float64)):
+                a = np.zeros(nsub, dtype=dt)
+                a[ok] = mjd[i]
+                parts.append(a)
+            valid = np.zeros(nsub, dtype=bool)
+            valid[ok] = True
+            TOAs = MJDArray(*parts, valid=valid)
+        TOA_errs = np.zeros(nsub, dtype="object")
+        TOA_errs[ok] = cat("TOA_err")
+        job.nu_fits_a[ok] = cat("nu_fit")  # (computed by whichever rank read the subint)
+        # the reference's list(np.zeros([nsub, 3])) with ok rows filled
+        # (pptoas.py:283-284, 406, 527-530) as one [nsub, 3] array: indexed
+        # by subint it gives the same rows
+        nu_fits = job.nu_fits_a
+        nu_refs = np.zeros((nsub, 3))
+        nu_refs[ok] = cat("nu_out")
+        for sh in shards:
+            self.TOA_list.add_block(sh.block)
         # DeltaDM weighted mean per archive (pptoas.py:664-681)
         DeltaDMs = DMs - job.DM0
         w = DM_errs[ok] ** -2 if np.all(DM_errs[ok]) else np.ones(nok)
@@ -1084,55 +1216,26 @@ class GetTOAs:
             print("Med. TOA error is %.3f us" % (np.median(phi_errs[ok]) *
                                                  data.Ps.mean() * 1e6))
 
-    def _make_toas(self, toas, pat, ff, colv, common, cov01, gof, tail, extra, name, tel, tcode,
-                   freq, toa_mjds, terr, dmo, dmeo):
-        """TOA records into toas[j], one key list per (fit flags, phi_DM_cov
-        present) pattern; flags in the reference's insertion order
-        (pptoas.py:606-661), then the additional flags."""
-        xk = [k for k, _ in extra]
-        xv = [v for _, v in extra]
-        for code in np.unique(pat).tolist():
-            rows = np.flatnonzero(pat == code).tolist()
-            f5 = ff[rows[0]]
-            keys = []
-            if f5[2]:
-                keys += ["gm", "gm_err"]
-            if f5[3]:
-                keys += (["scat_time", "log10_scat_time", "log10_scat_time_err"]
-                         if self.log10_tau else ["scat_time", "scat_time_err"])
-                keys += ["scat_ref_freq", "scat_ind"]
-            if f5[4]:
-                keys += ["scat_ind_err"]
-            vals = [colv[k] for k in keys]
-            keys += [k for k, _ in common]
-            vals += [v for _, v in common]
-            if code & 1:
-                keys.append("phi_DM_cov")
-                vals.append(cov01)
-            keys.append("gof")
-            vals.append(gof)
-            keys += [k for k, _ in tail]
-            vals += [v for _, v in tail]
-            if len(rows) != len(toas):
-                vals = [[v[j] for j in rows] for v in vals]
-            has_dm = bool(f5[1])
-            new = object.__new__
-            for j, row in zip(rows, zip(*vals)):
-                flags = dict(zip(keys, row))
-                if xk:
-                    flags.update(zip(xk, xv))
-                # TOA(name, freq, mjd, err, tel, tcode, DM, DM_err, flags) without the call
-                t = new(TOA)
-                t.archive = name
-                t.frequency = freq[j]
-                t.MJD = toa_mjds[j]
-                t.TOA_error = terr[j]
-                t.telescope = tel
-                t.telescope_code = tcode
-                t.DM = dmo[j] if has_dm else None
-                t.DM_error = dmeo[j] if has_dm else None
-                t.flags = flags
-                toas[j] = t
+
+class _Job(DataBunch):
+    """One archive's get_TOAs set-up (GetTOAs._prepare)."""
+
+    def row(self, key, s):
+        """Per-subint [nsub, nchan] input key ("freqs", "weights", "mask")
+        for subints s: one shared [nchan] row when every subint's is the
+        same."""
+        a = self.mask if key == "mask" else self.data[key]
+        if self.uniform[key]:
+            return a[0]
+        return _take(a, s)
+
+
+def _take(a, s):
+    """a[s]: a view when s is an ascending run of consecutive indices."""
+    s = np.asarray(s)
+    if len(s) and s[-1] - s[0] + 1 == len(s) and (len(s) < 3 or s[1] == s[0] + 1):
+        return a[int(s[0]):int(s[-1]) + 1]
+    return a[s]
 
 
 _RESULT_KEYS = ["params", "param_errs", "nu_out", "cov", "scales", "scale_errs",

@@ -87,11 +87,13 @@ def fit_portraits_batch(data, model, init, P, freqs, nu_fits=None, nu_outs=None,
                         is_toa=True, chan_mask=None, weights=None, model_idx=None,
                         guess=False, guess_Ns=100, guess_wrap=True, guess_nu=None,
                         guess_tau=None, method="trust-ncg", bounds=None, device=None,
-                        to_host=True):
+                        to_host=True, host_keys=None):
     """Batched fit_portrait_full over subints; returns arrays keyed like its DataBunch.
 
     method selects the device solver as minimize(method=...) does in the
-    reference (pptoaslib.py:995-1014); bounds are applied by TNC only."""
+    reference (pptoaslib.py:995-1014); bounds are applied by TNC only.
+    host_keys: the result keys to copy to the host (None: all) -- one
+    packed D2H (engine.results_to_host)."""
     if method not in ("trust-ncg", "TNC", "Newton-CG", "TNC-legacy"):
         print("Method '%s' is not implemented." % method)
         sys.exit()
@@ -117,9 +119,32 @@ def fit_portraits_batch(data, model, init, P, freqs, nu_fits=None, nu_outs=None,
         out = eng.fit_batch(data, model, freqs, P, init, fit_flags, **kw)
     if not to_host:
         return out
-    res = {k: v.cpu().numpy() for k, v in out.items() if not k.startswith("_")}
-    res["duration"] = np.full(len(res["chi2"]), (time.time() - t0) / max(len(res["chi2"]), 1))
+    from .engine import results_to_host
+    res = results_to_host(out, host_keys, eng.stream)
+    n = int(out["status"].shape[0])
+    res["duration"] = np.full(n, (time.time() - t0) / max(n, 1))
     return res
+
+
+class SyncPipeline:
+    """engine.FitPipeline's interface over a fit_portraits_batch-style
+    function, run at submit (the CPU tests' stand-in for the device)."""
+
+    def __init__(self, fit_fn, keys=None):
+        self.fit_fn, self.keys, self.pending = fit_fn, keys, []
+
+    def __len__(self):
+        return len(self.pending)
+
+    def submit(self, tag, data, model, freqs, P, init, fit_flags, nu_fit=None, nu_out=None,
+               **kw):
+        res = self.fit_fn(data, model, init, P, freqs, nu_fits=nu_fit, nu_outs=nu_out,
+                          fit_flags=fit_flags, **kw)
+        self.pending.append((tag, {k: np.asarray(v) for k, v in res.items()
+                                   if self.keys is None or k in self.keys}))
+
+    def collect(self):
+        return self.pending.pop(0)
 
 
 def _fit_batch_host(data, model, init, P, freqs, nu_fits, nu_outs, errs, fit_flags,

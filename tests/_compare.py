@@ -25,3 +25,22 @@ def phase_gap(phi, DM, GM, nu_DM, nu_GM, ref, P):
     p = phi_at(phi, DM, GM, nu_DM, nu_GM, ref["nu_DM"], ref["nu_GM"], P)
     d = abs(p - ref["phi"])
     return min(d, 1.0 - d) / ref["phi_err"]
+
+
+def tim_lines(gt):
+    """The .tim lines of gt.TOA_list as write_TOAs writes them (the native
+    writer over the column-built records, none built as objects yet), held
+    equal to toa_line over the TOA objects (which builds them)."""
+    import os
+    import tempfile
+    from pulseportraiture_amd import pplib
+    fd, path = tempfile.mkstemp(suffix=".tim")
+    os.close(fd)
+    try:
+        pplib.write_TOAs(gt.TOA_list, outfile=path, append=False)
+        bulk = open(path).read().splitlines()
+    finally:
+        os.unlink(path)
+    objs = [pplib.toa_line(t) for t in gt.TOA_list]
+    assert bulk == objs, "bulk .tim text differs from the per-TOA text"
+    return bulk

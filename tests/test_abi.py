@@ -52,3 +52,27 @@ def test_ppfits_library_exports_header():
     lib = psrfits.load_library()
     for s in syms:
         assert hasattr(lib, s), s
+
+
+def test_pptim_library_exports_header():
+    """libpptim.so (include/pptim.h, host .tim writer) exports every entry point."""
+    from pulseportraiture_amd import build, toas
+    build.build_tim()
+    txt = open(os.path.join(ROOT, "include", "pptim.h")).read()
+    syms = sorted(set(re.findall(r"^\s*(?:int|void|int64_t|const char\*)\s+(ppt_\w+)\s*\(",
+                                 txt, re.M)))
+    assert syms == sorted(["ppt_format_rows", "ppt_text_nparts", "ppt_text_part",
+                           "ppt_text_size", "ppt_text_rows", "ppt_text_free"])
+    lib = toas.load_tim_library()
+    for s in syms:
+        assert hasattr(lib, s), s
+
+
+def test_libraries_carry_source_hash():
+    """build.py reuses a library only when it carries today's source hash."""
+    from pulseportraiture_amd import build
+    build.build()
+    for path in (build.OUT, build.FITS_OUT, build.TIM_OUT):
+        assert not build.needs_build(path), path
+        cmd, deps = build._lib_specs()[path]
+        assert build.built_hash(path) == build.source_hash(cmd, deps)

@@ -3,7 +3,7 @@ range reads that touch only their rows, no file held open per archive, and
 get_TOAs reading a rank's shard in pieces of bounded size (VERDICT r03
 missing #3; pptoas.py:246,343 holds one archive at a time).
 
-The fit is replaced at the fit_portraits_batch boundary by the deterministic
+The fit is replaced at the fit_pipeline boundary by the deterministic
 stand-in of test_dist_drivers_cpu (no device)."""
 import os
 import resource
@@ -12,6 +12,8 @@ import numpy as np
 import pytest
 
 from tests.test_dist_drivers_cpu import DM0, fake_fit
+from tests._compare import tim_lines
+from pulseportraiture_amd.pptoaslib import SyncPipeline  # noqa: E402
 
 
 def _npz_archives(d, n, nsub=5, nchan=8, nbin=64):
@@ -32,7 +34,7 @@ def _npz_archives(d, n, nsub=5, nchan=8, nbin=64):
 
 def _get_toas(paths, monkeypatch, read_bytes_max=None):
     from pulseportraiture_amd import pplib, pptoas, synth
-    monkeypatch.setattr(pptoas, "fit_portraits_batch", fake_fit)
+    monkeypatch.setattr(pptoas, "fit_pipeline", lambda keys: SyncPipeline(fake_fit, keys))
     monkeypatch.setattr(pptoas, "gen_gaussian_portraits_device",
                         lambda code, params, alpha, nbin, freqs, nu_ref: np.array(
                             [pplib.gen_gaussian_portrait(code, params, alpha,
@@ -42,7 +44,7 @@ def _get_toas(paths, monkeypatch, read_bytes_max=None):
     if read_bytes_max is not None:
         gt.read_bytes_max = read_bytes_max
     gt.get_TOAs(quiet=True)
-    return [pplib.toa_line(t) for t in gt.TOA_list]
+    return tim_lines(gt)
 
 
 def test_npz_meta_reads_header_only_and_ranges(tmp_path, monkeypatch):

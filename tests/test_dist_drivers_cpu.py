@@ -3,7 +3,7 @@ its (archive, subint) units over ranks and gathers the results; ppalign
 shards its units and all-reduces the Fourier-domain portrait sum.
 
 The device calls are replaced at their boundaries by deterministic CPU
-stand-ins -- pptoas/ppalign.fit_portraits_batch (one result per subint that
+stand-ins -- pptoas.fit_pipeline / ppalign.fit_portraits_batch (one result per subint that
 depends only on that subint's inputs) and, for ppalign, an engine whose
 rotate_accumulate / irfft_rows are numpy (rfft * phasor, irfft).  What is
 checked is the N > 1 bookkeeping: every unit is fitted on exactly one rank,
@@ -16,6 +16,7 @@ import tempfile
 import numpy as np
 import torch
 import torch.multiprocessing as mp
+from pulseportraiture_amd.pptoaslib import SyncPipeline  # noqa: E402
 
 DM0 = 34.56789
 P0 = 1.0 / 345.67890123456789
@@ -97,7 +98,7 @@ def run_get_toas(log, reads=None, gather_to="root"):
     def fit(*a, **k):
         k["log_calls"] = log
         return fake_fit(*a, **k)
-    pptoas.fit_portraits_batch = fit
+    pptoas.fit_pipeline = lambda keys: SyncPipeline(fit, keys)
     # templates: the host restatement in place of the device generator
     pptoas.gen_gaussian_portraits_device = lambda code, params, alpha, nbin, freqs, nu_ref: \
         np.array([pplib.gen_gaussian_portrait(code, params, alpha, pplib.get_bin_centers(nbin), f,
@@ -105,10 +106,15 @@ def run_get_toas(log, reads=None, gather_to="root"):
     gt = pptoas.GetTOAs(names, synth.EXAMPLE_GMODEL, quiet=True)
     gt.gather_to = gather_to
     gt.get_TOAs(quiet=True)
+    # write_TOAs' bulk text first (no TOA object built yet), then the objects
+    with tempfile.NamedTemporaryFile("r", suffix=".tim") as f:
+        pplib.write_TOAs(gt.TOA_list, outfile=f.name, append=False)
+        gt.bulk_lines = f.read().splitlines()
     return [pplib.toa_line(t) for t in gt.TOA_list], gt
 
 
 def _toas_worker(rank, world, port, out_dir, gather_to):
+    from pulseportraiture_amd.toas import _as_bytes
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
@@ -116,9 +122,14 @@ def _toas_worker(rank, world, port, out_dir, gather_to):
         log, reads = [], []
         lines, gt = run_get_toas(log, reads, gather_to)
         subs = sorted((n, k) for n, lo, hi in reads for k in range(lo, hi))
+        own = gt.shard_blocks  # the TOA records this rank built for its own shard
         np.savez(os.path.join(out_dir, "toas%d.npz" % rank), lines=np.array(lines),
-                 nfit=sum(log), DeltaDM=np.array(gt.DeltaDM_means),
-                 read=np.array(["%s:%d" % x for x in subs]))
+                 bulk=np.array(gt.bulk_lines), nfit=sum(log), DeltaDM=np.array(gt.DeltaDM_means),
+                 read=np.array(["%s:%d" % x for x in subs]),
+                 own_rows=sum(b.n for b in own),
+                 own_subints=np.concatenate([[c.values for c in b.cols if c.key == "subint"][0]
+                                             for b in own]),
+                 own_text=np.array([_as_bytes(b.text[1]).decode() for b in own]))
     finally:
         torch.distributed.destroy_process_group()
 
@@ -143,11 +154,20 @@ def test_get_toas_sharded_ws2_equals_single_process(gather_to):
     # gather_to "root": rank 0 assembles every TOA in the reference's order and
     # the other ranks hold none; "all": every rank holds them
     holders = r if gather_to == "all" else r[:1]
+    assert gt.bulk_lines == ref_lines  # native .tim writer == per-TOA text
     for rk in holders:
         assert list(rk["lines"]) == ref_lines
+        assert list(rk["bulk"]) == ref_lines
         np.testing.assert_array_equal(rk["DeltaDM"], np.array(gt.DeltaDM_means))
     if gather_to == "root":
         assert len(r[1]["lines"]) == 0 and len(r[1]["DeltaDM"]) == 0
+    # every rank built its own shard's TOA records and .tim text: rank 1 the
+    # last 6 ok units (archive 1's subint 2, archive 2's 4 subints ... in
+    # unit order), and that text is exactly rank 0's lines for those units
+    assert int(r[0]["own_rows"]) == 6 and int(r[1]["own_rows"]) == 6
+    own = "".join(r[0]["own_text"]) + "".join(r[1]["own_text"])
+    assert own.splitlines() == ref_lines
+    assert "".join(r[1]["own_text"]).splitlines() == ref_lines[6:]
 
 
 # ---------------------------------------------------------------------------

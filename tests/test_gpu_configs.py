@@ -24,6 +24,7 @@ import pytest
 from tests.conftest import GOLDEN
 from tests.golden_consts import DM0
 from tests.test_gpu_drivers import mjd_diff_us, parse_tim
+from tests._compare import tim_lines
 
 pytestmark = pytest.mark.gpu
 
@@ -95,7 +96,7 @@ def test_get_toas_config_shapes(gpu, name, tmp_path):
     try:
         gt = pptoas.GetTOAs([name + ".fits"], "example.gmodel", quiet=True)
         gt.get_TOAs(quiet=True, **meta["kwargs"])
-        lines = [pplib.toa_line(t) for t in gt.TOA_list]
+        lines = tim_lines(gt)
     finally:
         os.chdir(cwd)
     p = name + "_"
@@ -211,7 +212,7 @@ def test_narrowband_toas_vs_reference(gpu):
                                                       weights=wts, DM=DM0))
         gt = pptoas.GetTOAs([name], "nbmodel.fits", quiet=True)
         gt.get_narrowband_TOAs(quiet=True)
-        lines = [pplib.toa_line(t) for t in gt.TOA_list]
+        lines = tim_lines(gt)
         p = name.split(".")[0] + "_"
         err = z[p + "phi_errs"]
         fitted = err > 0
@@ -288,7 +289,7 @@ def test_get_toas_config1_example_shape(gpu, tmp_path):
     try:
         gt = pptoas.GetTOAs(names, "example.gmodel", quiet=True)
         gt.get_TOAs(quiet=True)
-        lines = [pplib.toa_line(t) for t in gt.TOA_list]
+        lines = tim_lines(gt)
     finally:
         os.chdir(cwd)
     assert len(lines) == 49

@@ -13,6 +13,7 @@ import tempfile
 
 import numpy as np
 import pytest
+from tests._compare import tim_lines
 
 pytestmark = pytest.mark.gpu
 
@@ -53,7 +54,7 @@ def _run():
     names = _archives()
     gt = pptoas.GetTOAs(names, synth.EXAMPLE_GMODEL, quiet=True)
     gt.get_TOAs(quiet=True)
-    lines = [pplib.toa_line(t) for t in gt.TOA_list]
+    lines = tim_lines(gt)
     port = ppalign.align_archives(names, "gdist_guess.npz", fit_dm=True, niter=2, quiet=True)
     return lines, np.array(gt.DeltaDM_means), port
 

@@ -16,6 +16,7 @@ import pytest
 
 from tests.conftest import GOLDEN
 from tests.golden_consts import DM0
+from tests._compare import tim_lines
 
 pytestmark = pytest.mark.gpu
 
@@ -72,7 +73,7 @@ def test_get_toas_tim_lines(gpu, tag, tmp_path):
     try:
         gt = pptoas.GetTOAs(["synthA.fits", "synthB.fits"], "example.gmodel", quiet=True)
         gt.get_TOAs(quiet=True, **meta[tag]["kwargs"])
-        lines = [pplib.toa_line(t) for t in gt.TOA_list]
+        lines = tim_lines(gt)
     finally:
         os.chdir(cwd)
     ref = meta[tag]["tim"]

@@ -17,6 +17,7 @@ import pytest
 
 from tests.conftest import GOLDEN
 from tests.test_gpu_configs import compare_tim, register_synth_archive
+from tests._compare import tim_lines
 
 pytestmark = pytest.mark.gpu
 
@@ -92,7 +93,7 @@ def test_get_toas_templates(gpu, fx, tag, tmp_path):
         if m["ird"] is not None:
             gt.ird = gt.instrumental_response_dict = dict(m["ird"])
         gt.get_TOAs(quiet=True, **m["kwargs"])
-        lines = [pplib.toa_line(t) for t in gt.TOA_list]
+        lines = tim_lines(gt)
     finally:
         os.chdir(cwd)
     p = "gt_%s_" % tag

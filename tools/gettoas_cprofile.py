@@ -1,10 +1,8 @@
-"""cProfile of GetTOAs.get_TOAs + write_TOAs on the bench's registered
-10,000 x 64 x 2048 device-resident archive (the get_toas leg of bench.py):
-where the host time goes beside the ~9 ms of fits.  Diagnostic."""
+"""cProfile (tottime) of GetTOAs.get_TOAs + write_TOAs on the bench's
+registered 10,000 x 64 x 2048 device-resident archive.  Diagnostic."""
 import cProfile
 import pstats
 import sys
-import time
 
 import numpy as np
 import torch
@@ -15,6 +13,8 @@ from pulseportraiture_amd.engine import get_engine  # noqa: E402
 from pulseportraiture_amd.mjd import MJD  # noqa: E402
 
 nsub = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
+if len(sys.argv) > 2:
+    pptoas.GetTOAs.pipeline_fracs = tuple(float(x) for x in sys.argv[2].split(","))
 eng = get_engine(0)
 w = synth.make_workload(nsub, 64, 2048, seed=20240917)
 data = eng.synth(w.template, w.phase, w.sigma, w.seed, sub0=w.sub0)
@@ -28,16 +28,14 @@ def run():
     gt = pptoas.GetTOAs(["gt"], synth.EXAMPLE_GMODEL, quiet=True)
     gt.get_TOAs(quiet=True)
     pplib.write_TOAs(gt.TOA_list, outfile="/tmp/gt.tim", append=False)
-    return gt
 
 
-run()
-torch.cuda.synchronize()
-for _ in range(2):
-    t0 = time.perf_counter()
+for _ in range(3):
     run()
-    torch.cuda.synchronize()
-    print("call %.1f ms" % ((time.perf_counter() - t0) * 1e3))
-cProfile.run("run(); torch.cuda.synchronize()", "/tmp/gt.prof")
-pstats.Stats("/tmp/gt.prof").sort_stats("tottime").print_stats(25)
-pstats.Stats("/tmp/gt.prof").sort_stats("cumtime").print_stats(25)
+torch.cuda.synchronize()
+pr = cProfile.Profile()
+pr.enable()
+for _ in range(5):
+    run()
+pr.disable()
+pstats.Stats(pr).sort_stats("tottime").print_stats(45)

@@ -2,10 +2,11 @@
 """Host-side cost of GetTOAs.get_TOAs with the device fit stubbed out.
 
 Registers one archive of NSUB subints x 64 chan x NBIN bins (the data are
-never read by the stub), replaces pptoas.fit_portraits_batch with a function
+never read by the stub), replaces pptoas.fit_pipeline with a synchronous pipeline over a function
 that returns result arrays of the right shapes at zero cost, and times
 get_TOAs end to end (metadata, per-subint set-up, TOA records) plus the .tim
-text of every TOA.  usage: host_driver_bench.py [NSUB] [NBIN]
+text of every TOA (write_TOAs' bulk writer, checked against the per-TOA
+toa_line text).  usage: host_driver_bench.py [NSUB] [NBIN]
 """
 import os
 import sys
@@ -18,7 +19,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def stub_fit(data, model, init, P, freqs, nu_fits=None, nu_outs=None, errs=None,
              fit_flags=(1, 1, 0, 0, 0), chan_mask=None, **kw):
-    n, nchan = np.shape(freqs)
+    n, nchan = np.shape(data)[:2]
     init = np.asarray(init, dtype=np.float64)
     cov = np.zeros((n, 5, 5))
     cov[:, 0, 0], cov[:, 1, 1], cov[:, 0, 1] = 1e-8, 4e-8, 1e-9
@@ -32,6 +33,7 @@ def stub_fit(data, model, init, P, freqs, nu_fits=None, nu_outs=None, errs=None,
 
 def main():
     from pulseportraiture_amd import archive, pplib, pptoas, synth
+    from pulseportraiture_amd.pptoaslib import SyncPipeline
     from pulseportraiture_amd.mjd import MJD
     nsub = int(sys.argv[1]) if len(sys.argv) > 1 else 2000
     nbin = int(sys.argv[2]) if len(sys.argv) > 2 else 2048
@@ -41,7 +43,7 @@ def main():
     archive.register_archive("hostbench.fits", dict(
         subints=sub, freqs=w.freqs, Ps=np.full(nsub, w.P),
         epochs=[MJD(57000.0 + 1e-3 * k) for k in range(nsub)], DM=w.DM0))
-    pptoas.fit_portraits_batch = stub_fit
+    pptoas.fit_pipeline = lambda keys: SyncPipeline(stub_fit, keys)
     pptoas.gen_gaussian_portraits_device = lambda code, params, alpha, nb, freqs, nu_ref: \
         np.zeros((len(np.atleast_2d(freqs)), nchan, nb))
     # warm-up on the same archive: numpy / module first-use costs are per process
@@ -50,9 +52,14 @@ def main():
     t0 = time.perf_counter()
     gt.get_TOAs(quiet=True)
     t1 = time.perf_counter()
-    lines = [pplib.toa_line(t) for t in gt.TOA_list]
+    pplib.write_TOAs(gt.TOA_list, outfile="/tmp/hostbench.tim", append=False)
     t2 = time.perf_counter()
+    lines = open("/tmp/hostbench.tim").read().splitlines()
     assert len(lines) == nsub
+    slow = [pplib.toa_line(t) for t in gt.TOA_list]  # TOA objects, one line each
+    t3 = time.perf_counter()
+    assert slow == lines, "bulk .tim text differs from the per-TOA text"
+    print("per-TOA objects + toa_line: %.3f s" % (t3 - t2))
     print("nsub %d: get_TOAs %.3f s (%.0f TOAs/s), .tim text %.3f s (%.0f lines/s), "
           "together %.0f TOAs/s" % (nsub, t1 - t0, nsub / (t1 - t0), t2 - t1,
                                     nsub / (t2 - t1), nsub / (t2 - t0)))
