@@ -509,7 +509,7 @@ def main():
     legs = None
     if rank == 0 and world == 1 and config == "headline" and not args.no_legs:
         legs = {}
-        g, gt = leg_get_toas(eng, w, data)
+        g, gt = leg_get_toas(eng, w, data, reps=5)
         g["max_dphi_over_sigma_vs_fit_batch"] = float(np.max(
             np.abs(np.asarray(gt.phis[0]) - host["params"][:, 0]) / host["param_errs"][:, 0]))
         legs["get_toas"] = g

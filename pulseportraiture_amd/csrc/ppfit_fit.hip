@@ -142,12 +142,6 @@ __device__ __forceinline__ void block_sum_vec(double (&v)[N], double (*red)[48])
 // not one per step); the accumulation order is unchanged.
 constexpr int kPipe = 4;
 
-// Diagnostic builds only (tools/build_variant.py -DPPF_PROBE_SCAT=N, timing
-// of the scattering sweep's parts; results are wrong): 1 skips the
-// per-channel f/g/H terms, 2 the cell loop.
-#ifndef PPF_PROBE_SCAT
-#define PPF_PROBE_SCAT 0
-#endif
 // cells in flight per lane in the scattering sweep and k_scat_sweep's
 // workgroups per CU (launch bound); A/B knobs for diagnostic builds
 #ifndef PPF_SCAT_U
@@ -452,37 +446,8 @@ __device__ __forceinline__ double mode0_term(const ChanDeriv& d, const LanePick&
   return (on && t < 21) ? v : 0.0;
 }
 
-#ifndef PPF_POST_SPREAD
-#define PPF_POST_SPREAD 0  // A/B knob: k_post's with-scales terms over 8 lanes
-#endif
 #ifndef PPF_POST_WG_PER_CU
 #define PPF_POST_WG_PER_CU 2  // k_post<false>'s launch bound (A/B knob)
-#endif
-#if PPF_POST_SPREAD
-// MODE-1 (with-scales) cross term i: -2 (dC_i - C/S dS_i)
-__device__ __forceinline__ double mode1_cross(const ChanDeriv& d, const LanePick& L, double sc,
-                                              int i) {
-#pragma clang fp contract(off)
-  return -2.0 * (dCr(d, L, i) - sc * dSr(d, L, i));
-}
-// with-scales slot t (pair p = t mod 15 of block t / 15); R = t / 8
-template <int R>
-__device__ __forceinline__ double mode1_term(const ChanDeriv& d, const LanePick& L, double q,
-                                             double sc, double ic, int t, int fm) {
-#pragma clang fp contract(off)
-  constexpr int lo = (8 * R) / 15, hi = (8 * R + 7) / 15 < 2 ? (8 * R + 7) / 15 : 2;
-  const int b = t / 15, p = t - 15 * b;
-  const int pi = p < 5 ? 0 : (p < 9 ? 1 : (p < 12 ? 2 : (p < 14 ? 3 : 4)));
-  const int pj = p < 5 ? p : (p < 9 ? p - 4 : (p < 12 ? p - 7 : (p < 14 ? p - 9 : 4)));
-  double v0 = 0.0, v1 = 0.0, v2 = 0.0;
-  if (lo <= 0 && hi >= 0)
-    v0 = -2.0 * q * ((d2Cr(d, L, pi, pj) / d.C) - (0.5 * d2Sr(d, L, pi, pj) / d.S));
-  if (lo <= 1 && hi >= 1)
-    v1 = mode1_cross(d, L, sc, pi) * mode1_cross(d, L, sc, pj) * ic;
-  if (lo <= 2 && hi >= 2) v2 = Hnr(d, L, pi, pj);
-  const double v = b == 0 ? v0 : (b == 1 ? v1 : v2);
-  return ((fm >> pi) & (fm >> pj) & 1) ? v : 0.0;
-}
 #endif
 
 // phi_n (pptoaslib.py:206-208), reduced to [0, 1)
@@ -761,11 +726,7 @@ __device__ __forceinline__ void sweep(const FitArgs& a, const Meta& m, int c, in
       const double2* Xr = a.X + ((size_t)c * a.nchan + n) * a.NHP;
       const double* M2r = a.M2 + ((size_t)midx * a.nchan + n) * a.NHP;
       const double taun = tau_lin * pow(fr / refs[2], prm[4]);
-      if (PPF_PROBE_SCAT == 2) {
-        for (int i = 0; i < NACC; ++i) acc[i] = 0.5 + taun * i;
-      } else {
-        cells_scat<PPF_SCAT_U>(Xr, M2r, J, h, phif, taun, acc);
-      }
+      cells_scat<PPF_SCAT_U>(Xr, M2r, J, h, phif, taun, acc);
     }
 #pragma unroll
     for (int i = 0; i < NACC; ++i) acc[i] = group8_sum(acc[i]);
@@ -786,7 +747,7 @@ __device__ __forceinline__ void sweep(const FitArgs& a, const Meta& m, int c, in
           double* dst = acc_slot + (size_t)j * NACC;
           for (int i = 0; i < NACC; ++i) dst[i] = acc[i];
         }
-        const bool on = valid && !(SCAT && PPF_PROBE_SCAT == 1);
+        const bool on = valid;
 #pragma unroll
         for (int r = 0; r < 3; ++r) {
           const double v = chan8_sum(on ? mode0_term(d, L, q, h + 8 * r, fm) : 0.0);
@@ -799,45 +760,10 @@ __device__ __forceinline__ void sweep(const FitArgs& a, const Meta& m, int c, in
         continue;
       }
     }
-#if PPF_POST_SPREAD
-    if constexpr (MODE == 1) {
-      if (lrow) {
-        // with-scales terms spread over the channel's 8 lanes (slots h,
-        // h + 8, ...; each lane adds its slots into the channel lane's LDS
-        // row, so every row sums the same terms in the same group order)
-        const ChanDeriv d = derive<SCAT>(acc, scat, m.pn[jj], m.iw2[jj], fr, prm, tau_lin, refs,
-                                         P, log10_tau, nullptr);
-        const double q = d.C * d.C / d.S;
-        const LanePick L{d.dph[0], d.dph[1], d.dph[2], d.dts[0],
-                         d.dts[1], d.d2ts[0], d.d2ts[1], d.d2ts[2]};
-        const double sc = d.C / d.S;
-        if (valid && h < 7) {
-          double* dst = a.wsc + ((size_t)c * a.nchan + j) * 8;
-          dst[h] = h == 0 ? sc : (h == 1 ? d.S : mode1_cross(d, L, sc, h - 2));
-        }
-        if (valid) {
-          const double ic = 1.0 / (2.0 * d.S);
-          double* row = lrow[w * 8 + g8];
-          auto add = [&](auto rc) {
-            constexpr int r = decltype(rc)::value;
-            const int t = h + 8 * r;
-            if (t < NP) row[t] += mode1_term<r>(d, L, q, sc, ic, t, fm);
-          };
-          add(std::integral_constant<int, 0>{});
-          add(std::integral_constant<int, 1>{});
-          add(std::integral_constant<int, 2>{});
-          add(std::integral_constant<int, 3>{});
-          add(std::integral_constant<int, 4>{});
-          add(std::integral_constant<int, 5>{});
-        }
-        continue;
-      }
-    }
-#endif
     double ct[NP];
 #pragma unroll
     for (int i = 0; i < NP; ++i) ct[i] = 0.0;
-    if (h == 0 && valid && !(SCAT && PPF_PROBE_SCAT == 1)) {
+    if (h == 0 && valid) {
       const double dpre[2] = {m.d1[j], m.d2[j]};
       const ChanDeriv d = derive<SCAT>(acc, scat, m.pn[j], m.iw2[j], fr, prm, tau_lin, refs, P,
                                        log10_tau, MODE == 0 ? dpre : nullptr);

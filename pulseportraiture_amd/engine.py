@@ -803,6 +803,7 @@ class FitPipeline:
         self.pending = collections.deque()
         self.copy = self.side = None
         self.slots = [None, None]  # (pinned, device buffer, h2d event, free event)
+        self.models = {}
         self.k = 0
 
     def __len__(self):
@@ -848,6 +849,11 @@ class FitPipeline:
         return dbuf[:n].view(hd.shape), i
 
     def submit(self, tag, data, model, freqs, P, init, fit_flags, **kw):
+        if isinstance(model, np.ndarray):  # one device copy per template array
+            hit = self.models.get(id(model))
+            if hit is None or hit[0] is not model:
+                hit = self.models[id(model)] = (model, _dev_f64(model, self.eng.device))
+            model = hit[1]
         slot = None
         if not isinstance(data, torch.Tensor) or data.device.type == "cpu":
             data, slot = self._stage(data)

@@ -7,6 +7,7 @@ and assembles TOA records, Doppler-corrected DMs, flags and the DeltaDM mean
 on the host.  Archives come from ``archive.load_data`` (PSRCHIVE is out of
 scope; see archive.py).
 """
+import gc
 import time
 
 import numpy as np
@@ -33,6 +34,24 @@ def _dist_info():
     if dist.is_available() and dist.is_initialized():
         return dist.get_rank(), dist.get_world_size()
     return 0, 1
+
+
+def _gc_paused(fn):
+    """Run fn with Python's cyclic collector paused: get_TOAs makes few
+    containers, but a full collection of the caller's heap (a torch process
+    holds ~10^5 objects) landing inside the call costs more than the call."""
+    import functools
+
+    @functools.wraps(fn)
+    def run(*a, **k):
+        on = gc.isenabled()
+        gc.disable()
+        try:
+            return fn(*a, **k)
+        finally:
+            if on:
+                gc.enable()
+    return run
 
 
 def fit_pipeline(keys):
@@ -75,8 +94,8 @@ class GetTOAs:
     # device-resident subints of one call are fitted in pieces of these
     # fractions (at least pipeline_min_subints in all), each piece's TOA
     # records built while the next runs; pipeline_depth fits in flight
-    pipeline_fracs = (0.45, 0.25, 0.15, 0.1, 0.05)
-    pipeline_min_subints = 2048
+    pipeline_fracs = (0.7, 0.3)
+    pipeline_min_subints = 4096
     pipeline_depth = 1
 
     def __init__(self, datafiles, modelfile, quiet=False):
@@ -241,6 +260,7 @@ class GetTOAs:
         b.subints = _arch.host_array(sub)
         return b
 
+    @_gc_paused
     def get_TOAs(self, datafile=None, tscrunch=False, nu_refs=None, DM0=None, bary=True,
                  fit_DM=True, fit_GM=False, fit_scat=False, log10_tau=True, scat_guess=None,
                  fix_alpha=False, print_phase=False, print_flux=False, print_parangle=False,
@@ -1161,7 +1181,8 @@ class GetTOAs:
         else:
             pfl, pfle = np.zeros((nsub, nchan)), np.zeros((nsub, nchan))
             fluxes, flux_errs, flux_freqs = np.zeros(nsub), np.zeros(nsub), np.zeros(nsub)
-        mjd = [np.concatenate([sh.mjd[i] for sh in shards]) for i in range(3)]
+        mjd = [shards[0].mjd[i] if len(shards) == 1 else
+               np.concatenate([sh.mjd[i] for sh in shards]) for i in range(3)]
         if dense:
             TOAs = MJDArray(*mjd)
         else:
@@ -1173,9 +1194,13 @@ class GetTOAs:
             valid = np.zeros(nsub, dtype=bool)
             valid[ok] = True
             TOAs = MJDArray(*parts, valid=valid)
-        TOA_errs = np.zeros(nsub, dtype="object")
-        TOA_errs[ok] = cat("TOA_err")
-        job.nu_fits_a[ok] = cat("nu_fit")  # (computed by whichever rank read the subint)
+        if dense:
+            TOA_errs = cat("TOA_err").astype(object)
+            job.nu_fits_a[:] = cat("nu_fit")
+        else:
+            TOA_errs = np.zeros(nsub, dtype="object")
+            TOA_errs[ok] = cat("TOA_err")
+            job.nu_fits_a[ok] = cat("nu_fit")  # (computed by whichever rank read the subint)
         # the reference's list(np.zeros([nsub, 3])) with ok rows filled
         # (pptoas.py:283-284, 406, 527-530) as one [nsub, 3] array: indexed
         # by subint it gives the same rows
@@ -1186,11 +1211,12 @@ class GetTOAs:
             self.TOA_list.add_block(sh.block)
         # DeltaDM weighted mean per archive (pptoas.py:664-681)
         DeltaDMs = DMs - job.DM0
-        w = DM_errs[ok] ** -2 if np.all(DM_errs[ok]) else np.ones(nok)
-        mean, wsum = np.average(DeltaDMs[ok], weights=w, returned=True)
+        dd, de = (DeltaDMs, DM_errs) if dense else (DeltaDMs[ok], DM_errs[ok])
+        w = de ** -2 if np.all(de) else np.ones(nok)
+        mean, wsum = np.average(dd, weights=w, returned=True)
         var = wsum ** -1
         if nok > 1:
-            var *= np.sum(((DeltaDMs[ok] - mean) ** 2) * w) / (len(DeltaDMs[ok]) - 1)
+            var *= np.sum(((dd - mean) ** 2) * w) / (len(dd) - 1)
         for attr, val in [("order", datafile), ("obs", job.obs),
                           ("doppler_fs", data.doppler_factors), ("nu0s", data.nu0),
                           ("nu_fits", nu_fits), ("nu_refs", nu_refs), ("ok_isubs", ok),

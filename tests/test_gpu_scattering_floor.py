@@ -30,6 +30,15 @@ Asserted, per subint:
   the reference than the reference's own spread;
 * where the reference's own spread is below 1e-3 sigma, within 1e-3 sigma of
   the reference.
+And over the set, a bar that does not move with the device's results:
+* the alternate set is frozen at the 4 restarts + 24 reorderings committed
+  in r04 (asserted: 24 orderings);
+* the device agrees with the reference (within 1e-3 sigma) on at least as
+  many subints as the reference agrees with itself under its *worst* channel
+  ordering -- min over the 24 orderings of the fraction of subints whose
+  reordered end point is within 1e-3 sigma of the unpermuted one (0.87 on
+  this fixture).  The device is held to be no worse a summation order than
+  any of the reference's own.
 """
 import os
 
@@ -105,3 +114,12 @@ def test_scattering_200_subints_vs_reference(gpu):
     assert (near | on_alt | within).all(), np.where(~(near | on_alt | within))
     stable = spread <= 1e-3
     assert near[stable].all(), np.where(stable & ~near)
+    # the statistical bar: the reference's own agreement rate per ordering
+    assert int(zp["nperm"]) == 24
+    perm = np.stack([np.stack([zp["perm_" + c][:, k] for c in PARAMS], 1)
+                     for k in range(int(zp["nperm"]))], 1)  # [nsub, 24, 4]
+    self_rate = ((np.abs(perm - ref[:, None]) / sig[:, None]).max(axis=2) <= 1e-3).mean(axis=0)
+    print("agreement within 1e-3 sigma: device %.3f; reference with itself per ordering: "
+          "min %.3f, mean %.3f, max %.3f" % (near.mean(), self_rate.min(), self_rate.mean(),
+                                             self_rate.max()))
+    assert near.mean() >= self_rate.min(), (near.mean(), self_rate.min())

@@ -40,11 +40,11 @@ def timed(name, fn):
 E.Engine.fit_batch = timed("engine.fit_batch (launch)", E.Engine.fit_batch)
 E.FitPipeline.submit = timed("pipeline submit", E.FitPipeline.submit)
 E.FitPipeline.collect = timed("pipeline collect (wait)", E.FitPipeline.collect)
-for fr in [None, (1.0,), (0.5, 0.5), (0.45, 0.25, 0.15, 0.1, 0.05), (0.3, 0.25, 0.2, 0.15, 0.1)]:
+for fr in [None, (1.0,), (0.8, 0.2), (0.6, 0.25, 0.15), (0.3, 0.25, 0.2, 0.15, 0.1), (0.7, 0.3)]:
   if fr is not None:
     pptoas.GetTOAs.pipeline_fracs = fr
   print("pipeline_fracs", pptoas.GetTOAs.pipeline_fracs)
-  for rep in range(3):
+  for rep in range(4):
       sync()
       t0 = time.perf_counter()
       gt = pptoas.GetTOAs(["gt"], synth.EXAMPLE_GMODEL, quiet=True)
