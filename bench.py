@@ -47,13 +47,16 @@ CONFIGS = {
                    "config 3: 1000 subints x 512 chan x 1024 bin, phase+DM+tau+alpha (log10 tau)"),
     "gm": (2000, 128, 2048, [1, 1, 1, 0, 0], 0.0, False, 0.0,
            "config 4 slice: 128 chan x 2048 bin, phase+DM+GM (per-GPU shard batch)"),
+    "gm_shard": (125000, 128, 2048, [1, 1, 1, 0, 0], 0.0, False, 0.0,
+                 "config 4 per-GPU shard: 125000 subints x 128 chan x 2048 bin, phase+DM+GM, "
+                 "generated on the device chunk by chunk inside the timed region"),
     "get_toas": (10000, 64, 2048, [1, 1, 0, 0, 0], 0.0, False, 0.0,
                  "GetTOAs.get_TOAs end to end: registered 10000 x 64 x 2048 archive, "
                  "TOA records + .tim text"),
     "ppalign": (4096, 256, 2048, [1, 1, 0, 0, 0], 0.0, False, 0.0,
                 "config 5: align_archives, 4096 archives x 256 chan x 2048 bin, niter 3"),
 }
-TIMING_KEY = {"headline": "headline", "get_toas": "headline", "gm": "gm",
+TIMING_KEY = {"headline": "headline", "get_toas": "headline", "gm": "gm", "gm_shard": "gm",
               "scattering": "scattering", "ppalign": "ppalign"}
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
@@ -108,6 +111,8 @@ def parse():
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP events")
     ap.add_argument("--no-legs", action="store_true",
                     help="headline only: skip the get_toas / ppalign legs")
+    ap.add_argument("--shard-chunk", type=int, default=25000,
+                    help="gm_shard: subints generated and fitted per chunk")
     ap.add_argument("--ppalign-narch", type=int, default=4096)
     ap.add_argument("--ppalign-niter", type=int, default=3)
     ap.add_argument("--host-stream", type=int, default=None,
@@ -416,7 +421,7 @@ def main():
     fit_config = "headline" if config == "get_toas" else config
     if args.cpu_sample is None:
         args.cpu_sample = {"headline": 150, "gm": 60, "scattering": 4, "get_toas": 0,
-                           "ppalign": 0}[config]
+                           "ppalign": 0, "gm_shard": 16}[config]
     eng = Engine(local if world > 1 else 0)
     E._engines[eng.device.index] = eng  # the drivers' get_engine() uses this context
     for o in args.opt:
@@ -425,6 +430,8 @@ def main():
 
     if config == "ppalign":
         return main_ppalign(args, eng, rank, world)
+    if config == "gm_shard":
+        return main_gm_shard(args, eng, rank, world)
 
     # ---- synthetic inputs, resident in HBM before timing ----
     w, data, kw, tau_g = synth_inputs(eng, fit_config, nsub, args.seed, rank * nsub)
@@ -654,6 +661,156 @@ def roofline(args, config, nsub, nchan, nbin, flags, tau, ktimes, nfev):
         roof["frac"] = roof["achieved"] = None
         roof["invalid"] = "above peak"
     return roof, others
+
+def _oracle_fit(job):
+    """One oracle fit (bench parity samples; spawned worker)."""
+    os.environ["OMP_NUM_THREADS"] = "1"
+    from threadpoolctl import threadpool_limits
+    from oracle import cpu_baseline as CB
+    from pulseportraiture_amd import synth
+    port, nchan, nbin, seed, flags = job
+    w = synth.make_workload(1, nchan, nbin, seed=seed)
+    with threadpool_limits(limits=1):
+        r = CB.fit_subint(port, w, flags, False, 0.0, 0.0)
+    return np.asarray(r.params, dtype=float), np.asarray(r.param_errs, dtype=float), \
+        int(r.return_code)
+
+
+def main_gm_shard(args, eng, rank, world):
+    """--config gm_shard: one GPU's whole shard of BASELINE config 4
+    (1M subints x 128 x 2048 over 8 GPUs = 125,000 per GPU, 262 GB of
+    input -- more than HBM), fitted phase+DM+GM in chunks.  Inside the timed
+    region each chunk is generated on the device (k_synth: template, injected
+    phi / DM, Philox noise -- what reading the archives would put in HBM),
+    fitted, and its per-TOA results copied to pinned host memory; HIP events
+    split generation from fitting.  Beside it, the same run times the
+    2,000-subint slice (--config gm's step) to compare per-TOA rates, and
+    samples subints across the shard against the oracle."""
+    import torch
+    from pulseportraiture_amd import synth, pplib
+    nsub0, nchan, nbin, flags, _, _, _, desc = CONFIGS["gm_shard"]
+    N = args.nsub or nsub0
+    C = min(args.shard_chunk, N)
+    base = rank * N
+    dev = eng.device
+    w0 = synth.make_workload(1, nchan, nbin, seed=args.seed)
+    nu_fit = pplib.guess_fit_freq(w0.freqs)
+    model = torch.as_tensor(w0.model, device=dev)
+    freqs = torch.as_tensor(w0.freqs, device=dev)
+    starts = list(range(0, N, C))
+    # chunk metadata (injected phases per channel) on the host before timing
+    phases = [synth.make_workload(min(C, N - s0), nchan, nbin, seed=args.seed,
+                                  sub0=base + s0).phase for s0 in starts]
+    buf = torch.empty((C, nchan, nbin), dtype=torch.float64, device=dev)
+    P = torch.full((C,), w0.P, dtype=torch.float64, device=dev)
+    init = torch.tensor([[0.0, w0.DM0, 0.0, 0.0, 0.0]] * C, dtype=torch.float64, device=dev)
+    nu = torch.full((C, 3), nu_fit, dtype=torch.float64, device=dev)
+    small = ["params", "param_errs", "status", "nfev"]
+    host = {k: torch.empty((N,) + ((5,) if k.startswith("param") else ()),
+                           dtype=torch.float64 if k.startswith("param") else torch.int32,
+                           pin_memory=True) for k in small}
+    rng = np.random.default_rng(args.seed + rank)
+    S = max(0, args.cpu_sample) if world == 1 else 0
+    samp = np.sort(rng.choice(N, size=min(S, N), replace=False)) if S else np.zeros(0, int)
+    pport = torch.empty((max(len(samp), 1), nchan, nbin), dtype=torch.float64, pin_memory=True)
+    stream = torch.cuda.current_stream()
+    ev = []
+
+    def run(record):
+        for ci, s0 in enumerate(starts):
+            n = min(C, N - s0)
+            e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+            e0.record(stream)
+            eng.synth(w0.template, phases[ci], w0.sigma, args.seed, sub0=base + s0, out=buf[:n])
+            e1.record(stream)
+            out = eng.fit_batch(buf[:n], model, freqs, P[:n], init[:n], flags, nu_fit=nu[:n],
+                                guess=True, guess_Ns=100)
+            e2.record(stream)
+            for k in small:
+                host[k][s0:s0 + n].copy_(out[k], non_blocking=True)
+            if record:
+                ev.append((e0, e1, e2))
+                for j in np.flatnonzero((samp >= s0) & (samp < s0 + n)):
+                    pport[j].copy_(buf[int(samp[j]) - s0], non_blocking=True)
+        torch.cuda.synchronize()
+
+    # warm-up: one chunk (workspace and allocator at steady size)
+    eng.synth(w0.template, phases[0], w0.sigma, args.seed, sub0=base, out=buf[:min(C, N)])
+    eng.fit_batch(buf[:min(C, N)], model, freqs, P[:min(C, N)], init[:min(C, N)], flags,
+                  nu_fit=nu[:min(C, N)], guess=True, guess_Ns=100)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(True)
+    if world > 1:
+        torch.distributed.barrier()
+    t1 = time.perf_counter()
+    elapsed, rank_times = dist_times(t1 - t0, world, dev)
+    gen_ms = sum(a.elapsed_time(b) for a, b, _ in ev)
+    fit_ms = sum(b.elapsed_time(c) for _, b, c in ev)
+    status = host["status"].numpy()
+    nfev = host["nfev"].numpy()
+    # the 2,000-subint slice (--config gm's step) in the same process
+    wS, dS, kwS, _ = synth_inputs(eng, "gm", 2000, args.seed, base)
+    torch.cuda.synchronize()
+
+    def sstep():
+        return eng.fit_batch(dS, kwS["model"], kwS["freqs"], kwS["P"], kwS["init"], flags,
+                             nu_fit=kwS["nu"], guess=True, guess_Ns=100)
+    for _ in range(2):
+        sstep()
+    torch.cuda.synchronize()
+    ts0 = time.perf_counter()
+    for _ in range(10):
+        sstep()
+    torch.cuda.synchronize()
+    slice_ms = (time.perf_counter() - ts0) / 10 * 1e3
+    del dS
+    if rank != 0:
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
+    parity = None
+    if len(samp):
+        import multiprocessing as mp
+        jobs = [(pport[j].numpy().copy(), nchan, nbin, args.seed, flags) for j in range(len(samp))]
+        # the sample's ports were generated with sub0 = their global index:
+        # the oracle refits exactly those samples (CB.fit_subint: get_TOAs' guess + fit)
+        with mp.get_context("spawn").Pool(min(16, len(jobs))) as pool:
+            refs = pool.map(_oracle_fit, jobs)
+        hp, he = host["params"].numpy(), host["param_errs"].numpy()
+        gaps = {nm: float(max(abs(hp[i, j] - r[0][j]) / r[1][j] for i, r in zip(samp, refs)))
+                for j, nm in enumerate(["phi", "DM", "GM"])}
+        parity = {"sample": len(samp), "subints": [int(i) for i in samp],
+                  "tolerance": "1e-3 sigma (north_star)", "max_over_sigma": gaps,
+                  "status_match": bool(all(status[i] == r[2] for i, r in zip(samp, refs)))}
+    per_toa_us = elapsed / N * 1e6
+    line = {
+        "metric": "TOAs/sec (config 4 per-GPU shard, phase+DM+GM, 128ch x 2048bin fp64)",
+        "value": round(N * world / elapsed, 2), "unit": "TOAs/s", "n_gpus": world, "steps": 1,
+        "warmup": 1, "ms_per_step": round(elapsed * 1e3, 3),
+        "rank_ms_per_step": [round(t * 1e3, 3) for t in rank_times],
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic, generated on device chunk by chunk inside the timed region",
+        "config": {"workload": desc, "nsub_per_gpu": N, "chunk_subints": C, "chunks": len(starts),
+                   "nchan": nchan, "nbin": nbin, "fit_flags": flags, "guess_Ns": 100,
+                   "input_gb_per_gpu": round(N * nchan * nbin * 8 / 1e9, 1),
+                   "parallelism": "subint-sharded dp%d" % world},
+        "generate_ms": round(gen_ms, 2), "fit_ms": round(fit_ms, 2),
+        "fit_only_value": round(N / (fit_ms / 1e3), 2),
+        "per_toa_us": round(per_toa_us, 4), "fit_only_per_toa_us": round(fit_ms * 1e3 / N, 4),
+        "slice_2000": {"ms_per_step": round(slice_ms, 3),
+                       "per_toa_us": round(slice_ms * 1e3 / 2000, 4),
+                       "value": round(2000 / slice_ms * 1e3, 2)},
+        "fit_only_over_slice_per_toa": round(fit_ms / N / (slice_ms / 2000), 4),
+        "status_counts": {str(k): int(v) for k, v in zip(*np.unique(status, return_counts=True))},
+        "mean_nfev": float(np.mean(nfev)), "parity_sample": parity,
+    }
+    print(json.dumps(line))
+    if world > 1:
+        torch.distributed.destroy_process_group()
 
 
 def main_get_toas(args, eng, rank, world, w, data, step, desc):

@@ -50,10 +50,10 @@ def register_archive(name, bunch):
 class _Stack:
     """Archives registered together (register_archives) with one subints
     shape [nsub, npol, nchan, nbin]: their metadata arrays stacked on a
-    leading archive axis -- freqs / weights [narch, nsub, nchan], snrs0 and
-    noise0 (polarisation 0 of SNRs / noise_stds; noise0 NaN for the archives
-    without, has_noise [narch], None when none has them) [narch, nsub,
-    nchan], Ps [narch, nsub], DM [narch] --
+    leading archive axis -- freqs / weights [narch, nsub, nchan], snrs /
+    noise (SNRs / noise_stds [narch, nsub, npol, nchan]; noise NaN for the
+    archives without, has_noise [narch], None when none has them) and their
+    polarisation-0 views snrs0 / noise0, Ps [narch, nsub], DM [narch] --
     each archive's bunch holding views of its own row, and ``rows`` one
     [narch, nsub, npol, nchan, nbin] view of their subints when those are
     equally spaced views of one tensor (else None).  allok: every archive's
@@ -86,7 +86,13 @@ def register_archives(names, bunches):
     loadable under its own name exactly as if registered alone; when they all
     have one subints shape their metadata arrays are also stacked (_Stack), so
     a driver that opens every one of them indexes one array per key instead
-    of visiting each archive (ppalign's unit set-up)."""
+    of visiting each archive (ppalign's unit set-up).
+
+    The stacked keys (freqs, weights, Ps, SNRs, noise_stds) of each archive's
+    bunch are views of its stack row: change them in place.  Registered
+    bunches are otherwise frozen: a key *reassigned* after registration (or
+    a new DM) reaches the per-archive path only -- register the archives
+    again after such a change."""
     bs = [normalize(b, nm) for nm, b in zip(names, bunches)]
     for nm, b in zip(names, bs):
         _registry[nm] = b
@@ -101,26 +107,34 @@ def register_archives(names, bunches):
     try:
         stk.freqs = np.stack([b.freqs for b in bs])
         stk.weights = np.stack([b.weights for b in bs])
-        stk.snrs0 = np.stack([np.asarray(b.SNRs, dtype=np.float64)[:, 0] for b in bs])
+        stk.snrs = np.stack([np.asarray(b.SNRs, dtype=np.float64) for b in bs])
+        stk.snrs0 = stk.snrs[:, :, 0]
         stk.Ps = np.stack([b.Ps for b in bs])
         stk.DM = np.array([float(b.DM) for b in bs])
         stk.has_noise = np.array([b.noise_stds is not None for b in bs])
-        nan = np.full((nsub, nchan), np.nan)
-        stk.noise0 = np.stack([np.asarray(b.noise_stds, dtype=np.float64)[:, 0]
-                               if b.noise_stds is not None else nan for b in bs]) \
+        nan = np.full((nsub, npol, nchan), np.nan)
+        stk.noise = np.stack([np.asarray(b.noise_stds, dtype=np.float64)
+                              if b.noise_stds is not None else nan for b in bs]) \
             if stk.has_noise.any() else None
+        stk.noise0 = None if stk.noise is None else stk.noise[:, :, 0]
     except (ValueError, IndexError, TypeError):
         return list(names)
     if stk.freqs.shape != (len(bs), nsub, nchan) or stk.weights.shape != stk.freqs.shape or \
-            stk.snrs0.shape != stk.freqs.shape or stk.Ps.shape != (len(bs), nsub):
+            stk.snrs0.shape != stk.freqs.shape or stk.Ps.shape != (len(bs), nsub) or \
+            (stk.noise is not None and stk.noise.shape != stk.snrs.shape):
         return list(names)
     full = np.arange(nsub)
     stk.allok = all(len(b.ok_isubs) == nsub and np.array_equal(b.ok_isubs, full) and
                     all(len(oi) == nchan for oi in b.ok_ichans) for b in bs)
     stk.rows = _stacked_view([b.subints for b in bs])
     for i, b in enumerate(bs):
-        # the bunch's own arrays become views of its stack row (equal values)
+        # the bunch's own arrays become views of its stack row (equal values),
+        # so an in-place change reaches both the per-archive and the stacked
+        # paths
         b.freqs, b.weights, b.Ps = stk.freqs[i], stk.weights[i], stk.Ps[i]
+        b.SNRs = stk.snrs[i]
+        if b.noise_stds is not None:
+            b.noise_stds = stk.noise[i]
         b["_stack"] = (stk, i)
     return list(names)
 

@@ -93,7 +93,19 @@ class _All(np.ndarray):
     """Marker type of the shared every-channel index array (_units)."""
 
 
-ALL = None  # set per call: np.arange(nchan) viewed as _All
+_ALL_CACHE = {}
+
+
+def _all_index(nchan):
+    """The shared every-channel index array for nchan channels:
+    np.arange(nchan) viewed as _All, one read-only array per nchan (no
+    per-call module state: calls with different nchan do not interfere)."""
+    a = _ALL_CACHE.get(nchan)
+    if a is None:
+        a = np.arange(nchan).view(_All)
+        a.setflags(write=False)
+        a = _ALL_CACHE.setdefault(nchan, a)
+    return a
 
 
 class _Bulk:
@@ -204,7 +216,10 @@ class _Bulk:
             eq = ((b.F - mfq) == 0.0).all(axis=1)
         b.same = eq.reshape(n, nsub).all(axis=1)
         b.allok = stk.allok
-        if stk.rows is not None and stk.npol == 1:
+        if stk.rows is not None and stk.npol == 1 and isinstance(sel, slice):
+            # a view only: archives opened out of stack order would make this
+            # a device gather of every selected archive's subints on every
+            # rank; they take the per-archive rows instead
             b.rows_view = stk.rows[sel].reshape(R, nchan, stk.nbin)
         b.regs = [a.meta.subints for _, a in opened]
         b.index = {name: i for i, (name, _) in enumerate(opened)}
@@ -219,6 +234,7 @@ def _units(opened, model_data, bulk=None):
     units = []
     mf = model_data.freqs[0]
     nch = len(mf)
+    ALL = _all_index(nch)
     mok = model_data.ok_ichans[0]
     model_full = len(mok) == nch
     mfq = np.asarray(model_data.freqs)
@@ -269,6 +285,7 @@ def _units(opened, model_data, bulk=None):
 def _units_of(units, name, m, same, mf, mok, model_full):
     """One archive's units (see _units); same: its frequencies are the template's."""
     nch = len(mf)
+    ALL = _all_index(nch)
     for isub in m.ok_isubs:
         if same:
             oi = m.ok_ichans[isub]
@@ -599,8 +616,6 @@ def align_archives(metafile, initial_guess, fit_dm=True, tscrunch=False, pscrunc
     try:
         opened = _open_all(datafiles, model_data, SNR_cutoff, quiet, skip_these, tscrunch,
                            pscrunch)
-        global ALL
-        ALL = np.arange(nchan).view(_All)
         bulk = _Bulk.build(opened, model_data, nchan)
         units = _units(opened, model_data, bulk)
         t0 = mark("open", t0)
@@ -634,9 +649,10 @@ def align_archives(metafile, initial_guess, fit_dm=True, tscrunch=False, pscrunc
         tw = torch.zeros(nchan, dtype=torch.float64, device=dev)
         if stack is not None:
             stack.fit_and_accumulate(eng, model_port, fit_dm, accum, tw, mark)
+        t1 = t0 if stack is None else time.perf_counter()  # the 1-channel hack's start
         for u in single:  # 1-channel hack, ppalign.py:196-201
             _single_channel(u, archives, model_port, npol, accum, tw, dev)
-        t0 = mark("accumulate", t0 if stack is None else time.perf_counter())
+        t0 = mark("accumulate", t1)
         allreduce_sum(accum, tw)
         spec = torch.view_as_complex(accum).reshape(npol * nchan, nharm)
         port = eng.irfft_rows(spec, nbin).reshape(npol, nchan, nbin)

@@ -41,7 +41,6 @@ def _bunches(n, kind, rng):
 
 def _setup(names, model, bulk_on):
     opened = ppalign._open_all(names, model, 0.0, True, [], False, True)
-    ppalign.ALL = np.arange(NCHAN).view(ppalign._All)
     bulk = ppalign._Bulk.build(opened, model, NCHAN) if bulk_on else None
     units = ppalign._units(opened, model, bulk)
     multi = [u for u in units if len(u[2]) > 1]

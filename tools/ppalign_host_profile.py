@@ -42,7 +42,6 @@ def main():
         t = [time.perf_counter()]
         opened = ppalign._open_all(names, model, 0.0, True, [], False, True)
         t.append(time.perf_counter())
-        ppalign.ALL = np.arange(nchan).view(ppalign._All)
         bulk = None if "--slow" in sys.argv else ppalign._Bulk.build(opened, model, nchan)
         units = ppalign._units(opened, model, bulk)
         t.append(time.perf_counter())
