@@ -52,7 +52,8 @@ struct ppf_ctx {
   Buffer ptime;   // k_fit_taylor phase clocks (ppf_phase_profile)
   Buffer spart;   // split scattering solve: block partials + running count
   Buffer tmpl;    // template builders: knots / coefficients, rows and spectra
-  int* active_h = nullptr;  // pinned host copy of the running count
+  int* active_h = nullptr;  // pinned host copies of the running count (two in flight)
+  hipEvent_t scat_ev[2] = {nullptr, nullptr};  // their copies' completion
   hipStream_t stream2 = nullptr;        // second queue of the piece pipeline
   int pipe = 0;                         // pieces per chunk (0: default)
   std::vector<hipEvent_t> sync_events;  // ordering events (no timing)
@@ -292,6 +293,7 @@ void ppf_ctx_destroy(ppf_ctx* ctx) {
   if (ctx->spart.p) (void)hipFree(ctx->spart.p);
   if (ctx->tmpl.p) (void)hipFree(ctx->tmpl.p);
   if (ctx->active_h) (void)hipHostFree(ctx->active_h);
+  for (auto e : ctx->scat_ev) if (e) (void)hipEventDestroy(e);
   if (ctx->ws.p) (void)hipFree(ctx->ws.p);
   if (ctx->mspec.p) (void)hipFree(ctx->mspec.p);
   if (ctx->aux.p) (void)hipFree(ctx->aux.p);
@@ -549,9 +551,12 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   const int split = std::max(1, std::min(16, nchan / 64));
   if (split_scat) {
     if (int r = ensure(ctx, ctx->spart,
-                       (size_t)chunk * ((nchan + 7) / 8) * kScatPart * sizeof(double) + 256))
+                       (size_t)chunk * ((nchan + 7) / 8) * kScatPart * sizeof(double) +
+                           64 * sizeof(int) + 256))
       return r;
-    if (!ctx->active_h) HIPCHK(ctx, hipHostMalloc(&ctx->active_h, sizeof(int)));
+    if (!ctx->active_h) HIPCHK(ctx, hipHostMalloc(&ctx->active_h, 2 * sizeof(int)));
+    for (auto& e : ctx->scat_ev)
+      if (!e) HIPCHK(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
   const size_t lds_guess =
       (size_t)(NHP + (d->guess ? pfa_scratch_slots(d->guess_Ns, NH) : 0)) * sizeof(double2);
@@ -669,22 +674,26 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
         }))
       return r;
     if (split_scat && !tnc && !ncg) {
-      // k_solve<true> with each evaluation over `split` blocks per subint
+      // k_solve<true> with each evaluation over `cur` blocks per subint
+      // (k_scat_sweep) and then every subint's solver step (k_scat_step)
       double* part = static_cast<double*>(ctx->spart.p);
-      int* active = reinterpret_cast<int*>(part + (size_t)nc * ((nchan + 7) / 8) * kScatPart);
-      // the running count is read back every kCheck iterations (a finished
-      // subint's blocks exit at once, so the extra launches are cheap)
+      int* ctrs = reinterpret_cast<int*>(part + (size_t)nc * ((nchan + 7) / 8) * kScatPart);
+      HIPCHK(ctx, hipMemsetAsync(ctrs, 0, 2 * sizeof(int), ctx->stream));
+      // iterations go in groups of kCheck launches; after each group its
+      // running count is copied to pinned memory, and the host reads group
+      // g's count only once group g + 1 is queued behind it, so the device
+      // never waits for the host (a group launched after the last subint has
+      // finished costs kCheck near-empty grids)
       constexpr int kCheck = 4;
       // once few subints are left (the tail of slow fits), each sweep is
       // spread over more blocks: one 8-channel group per wave.  The group
       // partials, and so every result, do not depend on the split.
       int cur = split;
       const int split_tail = std::max(split, std::min(32, (nchan + 31) / 32));
-      // after the first kCheck iterations, each group of kCheck is one
-      // hipGraph launch (the same kernels in the same order, captured once
-      // per call and split): fewer launch gaps between the short kernels
+      // groups after the first are one hipGraph launch each (the same kernels
+      // in the same order, captured once per call and split)
       hipGraphExec_t gx[2] = {nullptr, nullptr};
-      auto graph_for = [&](int s, hipGraphExec_t* ex) -> int {
+      auto graph_for = [&](int sp, hipGraphExec_t* ex) -> int {
         if (*ex) return PPF_OK;
         // captured on the context's second queue (the context stream may be
         // the legacy default stream, which cannot capture); launched on the
@@ -695,10 +704,9 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
         hipGraph_t g = nullptr;
         HIPCHK(ctx, hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
         for (int k = 0; k < kCheck; ++k) {
-          hipLaunchKernelGGL(k_scat_sweep, dim3(nc, s), dim3(kBlock), lds_meta, cs, fa, part, s,
+          hipLaunchKernelGGL(k_scat_sweep, dim3(nc, sp), dim3(kBlock), lds_meta, cs, fa, part, sp,
                              0);
-          (void)hipMemsetAsync(active, 0, sizeof(int), cs);
-          hipLaunchKernelGGL(k_scat_step, dim3(nc), dim3(64), 0, cs, fa, part, split, 0, active);
+          hipLaunchKernelGGL(k_scat_step, dim3(nc), dim3(64), 0, cs, fa, part, 0, ctrs, k & 1);
         }
         HIPCHK(ctx, hipStreamEndCapture(cs, &g));
         const hipError_t e = hipGraphInstantiate(ex, g, nullptr, nullptr, 0);
@@ -719,32 +727,45 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
             if (g[i]) (void)hipGraphExecDestroy(g[i]);
         }
       } gfree{gx, ctx->stream};
-      for (int it = 0, init = 1;; ++it, init = 0) {
-        if (ctx->opt[PPF_OPT_SCAT_GRAPH] && it >= kCheck && it % kCheck == 0 && it + kCheck - 1 <= 1001) {
+      // group gi: iterations kCheck * gi ... + kCheck - 1 (the first is the
+      // init sweep); its count lands in active_h[gi & 1]
+      auto issue = [&](int gi) -> int {
+        const int it0 = kCheck * gi;
+        if (gi > 0 && ctx->opt[PPF_OPT_SCAT_GRAPH]) {
           hipGraphExec_t* ex = &gx[cur == split ? 0 : 1];
           if (int r = graph_for(cur, ex)) return r;
           if (int r = timed(ctx, PPF_K_SOLVE, [&] { (void)hipGraphLaunch(*ex, ctx->stream); }))
             return r;
-          it += kCheck - 1;
         } else {
-          if (int r = timed(ctx, PPF_K_SOLVE, [&] {
-                hipLaunchKernelGGL(k_scat_sweep, dim3(nc, cur), dim3(kBlock), lds_meta,
-                                   ctx->stream, fa, part, cur, init);
-              }))
-            return r;
-          HIPCHK(ctx, hipMemsetAsync(active, 0, sizeof(int), ctx->stream));
-          if (int r = timed(ctx, PPF_K_SOLVE, [&] {
-                hipLaunchKernelGGL(k_scat_step, dim3(nc), dim3(64), 0, ctx->stream, fa, part,
-                                   split, init, active);
-              }))
-            return r;
+          for (int k = 0; k < kCheck; ++k) {
+            const int init = it0 + k == 0 ? 1 : 0;
+            if (int r = timed(ctx, PPF_K_SOLVE, [&] {
+                  hipLaunchKernelGGL(k_scat_sweep, dim3(nc, cur), dim3(kBlock), lds_meta,
+                                     ctx->stream, fa, part, cur, init);
+                }))
+              return r;
+            if (int r = timed(ctx, PPF_K_SOLVE, [&] {
+                  hipLaunchKernelGGL(k_scat_step, dim3(nc), dim3(64), 0, ctx->stream, fa, part,
+                                     init, ctrs, (it0 + k) & 1);
+                }))
+              return r;
+          }
         }
-        if (it % kCheck != kCheck - 1 && it <= 1001) continue;
-        HIPCHK(ctx, hipMemcpyAsync(ctx->active_h, active, sizeof(int), hipMemcpyDeviceToHost,
-                                   ctx->stream));
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-        if (*ctx->active_h == 0 || it > 1001) break;  // trust-ncg stops at 1000 iterations
-        if (*ctx->active_h < ctx->opt[PPF_OPT_SCAT_TAIL]) cur = split_tail;
+        HIPCHK(ctx, hipMemcpyAsync(ctx->active_h + (gi & 1), ctrs + ((it0 + kCheck - 1) & 1),
+                                   sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, hipEventRecord(ctx->scat_ev[gi & 1], ctx->stream));
+        return PPF_OK;
+      };
+      // trust-ncg stops a fit at 1000 iterations (+ the init sweep)
+      const int max_groups = (1001 + kCheck) / kCheck + 1;
+      if (int r = issue(0)) return r;
+      for (int gi = 0;; ++gi) {
+        if (gi + 1 < max_groups)
+          if (int r = issue(gi + 1)) return r;
+        HIPCHK(ctx, hipEventSynchronize(ctx->scat_ev[gi & 1]));
+        const int running = ctx->active_h[gi & 1];
+        if (running == 0 || gi + 1 >= max_groups) break;
+        if (running < ctx->opt[PPF_OPT_SCAT_TAIL]) cur = split_tail;
       }
     }
     if (taylor) {

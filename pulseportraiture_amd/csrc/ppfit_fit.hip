@@ -208,6 +208,15 @@ __device__ __forceinline__ double rcp_nr(double d) {
 
 // U cells in flight per lane: 4 (measured on config 3: solve 20.8 ms with 2,
 // 19.9 with 4, 20.3 with 8, all at two waves per SIMD).
+//
+// The sweep is vector-issue bound (r04 SQ counters: the SIMDs' VALU issue
+// ~0.9 busy), so the loop carries no work that is not arithmetic on a cell:
+// the unrolled body covers whole blocks of 2U cells with unclamped,
+// unselected loads (constant offsets from one pointer per row), and the
+// J mod 2U cells past the last block (J = NHP / 8 is 2^m + 1 for a power-of-
+// two nbin: one cell) run one at a time after it.  Each cell's operations and
+// the order of the sums are those of the padded loop this replaced, minus
+// its zero cells, which only ever added +0.0.
 template <int U>
 __device__ __forceinline__ void cells_scat(const double2* __restrict__ Xr,
                                            const double* __restrict__ M2r, int J, int h,
@@ -215,67 +224,69 @@ __device__ __forceinline__ void cells_scat(const double2* __restrict__ Xr,
   const double2 step = turn_phasor(8.0, phif);
   const double itau = 1.0 / taun;
   const double w0 = kTwoPi * taun;
-  const double2 zero = cmk(0.0, 0.0);
   double2 e = cmk(1.0, 0.0);
   double a[NACC];
   for (int i = 0; i < NACC; ++i) a[i] = 0.0;
-  // cells j < Jpad (U-aligned; j >= J are zero cells, as before); two register
-  // sets of U cells alternate, each reloaded (clamped, unpredicated) right
-  // after it is consumed, so the loop carries no copies of in-flight loads
-  const int Jpad = (J + U - 1) / U * U;
-  double2 xa[U], xb[U];
-  double ma[U], mb[U];
-  auto load = [&](int jb, double2 (&x)[U], double (&m)[U]) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int j = min(jb + u, J - 1);
-      x[u] = Xr[h + 8 * j];
-      m[u] = M2r[h + 8 * j];
-    }
-  };
-  auto consume = [&](int jb, const double2 (&xs)[U], const double (&ms)[U]) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int jj = jb + u;
-      if (jj >= Jpad) break;
-      const int k = h + 8 * jj;
-      if ((jj & 31) == 0) e = turn_phasor((double)k, phif);
-      else e = cmul(e, step);
-      const bool ok = jj < J;
-      const double2 x = ok ? xs[u] : zero;
-      const double m2 = ok ? ms[u] : 0.0;
-      const double2 W = cmul(x, e);
-      const double kd = (double)k;
-      const double aa = w0 * kd;
-      const double id = rcp_nr(fma(aa, aa, 1.0));
-      const double2 B = cmk(id, -aa * id);
-      const double2 Bm1 = cmk(B.x - 1.0, B.y);
-      const double2 f = cscale(cmul(B, Bm1), itau);
-      const double2 g1 = cscale(cmul(f, Bm1), 2.0 * itau);
-      const double2 WB = cmulc(W, B);
-      const double2 Wf = cmulc(W, f);
-      const double2 Wg = cmulc(W, g1);
-      a[0] += WB.x;
-      a[1] = fma(kd, WB.y, a[1]);
-      a[2] = fma(kd * kd, WB.x, a[2]);
-      a[3] += Wf.x;
-      a[4] = fma(kd, Wf.y, a[4]);
-      a[5] += Wg.x;
-      a[6] = fma(cabs2(B), m2, a[6]);
-      a[7] = fma(fma(B.x, f.x, B.y * f.y), m2, a[7]);
-      a[8] = fma(cabs2(f), m2, a[8]);
-      a[9] = fma(fma(B.x, g1.x, B.y * g1.y), m2, a[9]);
-    }
+  const double2* __restrict__ xp = Xr + h;
+  const double* __restrict__ mp = M2r + h;
+  auto cell = [&](int jj, double2 x, double m2) {
+    const int k = h + 8 * jj;
+    if ((jj & 31) == 0) e = turn_phasor((double)k, phif);
+    else e = cmul(e, step);
+    const double2 W = cmul(x, e);
+    const double kd = (double)k;
+    const double aa = w0 * kd;
+    const double id = rcp_nr(fma(aa, aa, 1.0));
+    const double2 B = cmk(id, -aa * id);
+    const double2 Bm1 = cmk(B.x - 1.0, B.y);
+    const double2 f = cscale(cmul(B, Bm1), itau);
+    const double2 g1 = cscale(cmul(f, Bm1), 2.0 * itau);
+    const double2 WB = cmulc(W, B);
+    const double2 Wf = cmulc(W, f);
+    const double2 Wg = cmulc(W, g1);
+    a[0] += WB.x;
+    a[1] = fma(kd, WB.y, a[1]);
+    a[2] = fma(kd * kd, WB.x, a[2]);
+    a[3] += Wf.x;
+    a[4] = fma(kd, Wf.y, a[4]);
+    a[5] += Wg.x;
+    a[6] = fma(cabs2(B), m2, a[6]);
+    a[7] = fma(fma(B.x, f.x, B.y * f.y), m2, a[7]);
+    a[8] = fma(cabs2(f), m2, a[8]);
+    a[9] = fma(fma(B.x, g1.x, B.y * g1.y), m2, a[9]);
   };
   static_assert(32 % U == 0, "phasor re-seed every 32 cells");
-  load(0, xa, ma);
-  load(U, xb, mb);
-  for (int jb = 0; jb < Jpad; jb += 2 * U) {
+  const int Jmain = J / (2 * U) * (2 * U);  // cells of the unrolled blocks
+  int jb = 0;
+  if (Jmain >= 2 * U) {
+    // two register sets of U cells alternate, each reloaded right after it
+    // is consumed, so the loop carries no copies of in-flight loads
+    double2 xa[U], xb[U];
+    double ma[U], mb[U];
+    auto load = [&](int j0, double2 (&x)[U], double (&m)[U]) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        x[u] = xp[8 * (j0 + u)];
+        m[u] = mp[8 * (j0 + u)];
+      }
+    };
+    auto consume = [&](int j0, const double2 (&xs)[U], const double (&ms)[U]) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) cell(j0 + u, xs[u], ms[u]);
+    };
+    load(0, xa, ma);
+    load(U, xb, mb);
+    for (; jb + 4 * U <= Jmain; jb += 2 * U) {
+      consume(jb, xa, ma);
+      load(jb + 2 * U, xa, ma);
+      consume(jb + U, xb, mb);
+      load(jb + 3 * U, xb, mb);
+    }
     consume(jb, xa, ma);
-    load(jb + 2 * U, xa, ma);
     consume(jb + U, xb, mb);
-    load(jb + 3 * U, xb, mb);
+    jb += 2 * U;
   }
+  for (; jb < J; ++jb) cell(jb, xp[8 * jb], mp[8 * jb]);
   for (int i = 0; i < NACC; ++i) acc[i] = a[i];
 }
 
@@ -1466,52 +1477,52 @@ __device__ __forceinline__ bool scat_split_owner(const FitArgs& a, const SolveSt
   return a.method == PPF_METHOD_TRUST_NCG && st.scat != 0 && !st.sdone;
 }
 
-__global__ __launch_bounds__(kBlock, PPF_SCAT_WG_PER_CU) void k_scat_sweep(FitArgs a, double* part, int split,
-                                                       int init) {
-  extern __shared__ __align__(16) unsigned char dyn[];
-  __shared__ SolveShared sh;
-  const int c = blockIdx.x, q = blockIdx.y, s = a.sub0 + c, tid = threadIdx.x;
-  const SolveState& st = a.st[c];
-  if (!scat_split_owner(a, st)) return;
-  const Meta m = load_meta(a, c, s, dyn, &sh.nok);
-  if (m.nok == 0) return;
-  // channel range of this block: whole groups of 8, blocks in order; each
-  // group's wave-reduced terms go to part[c][group] (k_scat_step sums them
-  // in k_solve's order)
-  const int ng = (m.nok + 7) >> 3;
-  const int per = (ng + split - 1) / split;
-  const int j0 = q * per * 8, j1 = min(m.nok, (q + 1) * per * 8);
-  const double* prm = init ? st.x : st.xp;
-  const int slot = init ? 0 : (st.slot ^ 1);
-  double* acc = a.acc + ((size_t)c * 2 + slot) * a.nchan * NACC;
-  if (j0 < j1)
-    sweep<0, true>(a, m, c, s, prm, st.refs, a.P[s], acc, sh.out, sh.red, TaylorSrc{}, nullptr,
-                   j0, j1, part + (size_t)c * ((a.nchan + 7) >> 3) * kScatPart);
-}
-
-__global__ __launch_bounds__(64) void k_scat_step(FitArgs a, const double* part, int split,
-                                                  int init, int* active) {
-  __shared__ double out[kScatPart];
-  const int c = blockIdx.x, s = a.sub0 + c, lane = threadIdx.x;
+// The solver step of one subint (one wave, 64 lanes; out: kScatPart doubles
+// of LDS): the group partials summed in k_solve's order, then k_solve's
+// accept / reject and the next Steihaug proposal, the state in SolveState.
+__device__ __forceinline__ void scat_step_wave(const FitArgs& a, const double* part, int init,
+                                               int* active, double* out, int c) {
+  const int s = a.sub0 + c, lane = threadIdx.x & 63;
   SolveState& st = a.st[c];
-  if (!scat_split_owner(a, st)) return;
-  double cnt = 0.0;  // fitted channels
-  for (int n = lane; n < a.nchan; n += 64) cnt += (!a.mask || a.mask[(size_t)s * a.nchan + n]) ? 1.0 : 0.0;
-  const int nok = (int)wave_sum(cnt);
+  // fitted channels: the mask loads all in flight, then one count
+  int cnt = 0;
+#pragma unroll 8
+  for (int n0 = 0; n0 < a.nchan; n0 += 64) {
+    const int n = n0 + lane;
+    const bool ok = n < a.nchan && (!a.mask || a.mask[(size_t)s * a.nchan + n]);
+    cnt += __popcll(__ballot(ok));
+  }
+  const int nok = cnt;
   // group terms summed exactly as one k_solve block sums them: wave w's
-  // running sum over groups w, w + kWaves, ..., then the waves in order
+  // running sum over groups w, w + kWaves, ..., then the waves in order.
+  // The terms of kBatch groups are loaded before any is added, so the loads
+  // overlap instead of each waiting for the previous add (the additions, and
+  // so the sums, are unchanged)
   if (lane < 21) {
-    const double* pc = part + (size_t)c * ((a.nchan + 7) >> 3) * kScatPart;
+    const double* pc = part + (size_t)c * ((a.nchan + 7) >> 3) * kScatPart + lane;
     const int ng = (nok + 7) >> 3;
+    constexpr int kBatch = 16;
     double t = 0.0;
     for (int w = 0; w < kWaves; ++w) {
       double r = 0.0;
-      for (int gi = w; gi < ng; gi += kWaves) r += pc[(size_t)gi * kScatPart + lane];
+      for (int g0 = w; g0 < ng; g0 += kWaves * kBatch) {
+        double v[kBatch];
+#pragma unroll
+        for (int b = 0; b < kBatch; ++b) {
+          const int gi = min(g0 + kWaves * b, ng - 1);
+          v[b] = pc[(size_t)gi * kScatPart];
+        }
+#pragma unroll
+        for (int b = 0; b < kBatch; ++b)
+          if (g0 + kWaves * b < ng) r += v[b];
+      }
       t += r;
     }
     out[lane] = t;
   }
-  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   auto load_fgh = [&](double& ff, double& gg, double (&HH)[5]) {
     ff = out[0];
     gg = lane < 5 ? out[1 + lane] : 0.0;
@@ -1641,6 +1652,42 @@ __global__ __launch_bounds__(64) void k_scat_step(FitArgs a, const double* part,
       st.scat_post = tl != 0.0;
     }
   }
+}
+
+__global__ __launch_bounds__(kBlock, PPF_SCAT_WG_PER_CU) void k_scat_sweep(FitArgs a, double* part,
+                                                                          int split, int init) {
+  extern __shared__ __align__(16) unsigned char dyn[];
+  __shared__ SolveShared sh;
+  const int c = blockIdx.x, q = blockIdx.y, s = a.sub0 + c, tid = threadIdx.x;
+  const SolveState& st = a.st[c];
+  if (!scat_split_owner(a, st)) return;
+  const Meta m = load_meta(a, c, s, dyn, &sh.nok);
+  if (m.nok == 0) return;
+  // channel range of this block: whole groups of 8, blocks in order; each
+  // group's wave-reduced terms go to part[c][group] (k_scat_step sums them
+  // in k_solve's order)
+  const int ng = (m.nok + 7) >> 3;
+  const int per = (ng + split - 1) / split;
+  const int j0 = q * per * 8, j1 = min(m.nok, (q + 1) * per * 8);
+  const double* prm = init ? st.x : st.xp;
+  const int slot = init ? 0 : (st.slot ^ 1);
+  double* acc = a.acc + ((size_t)c * 2 + slot) * a.nchan * NACC;
+  if (j0 < j1)
+    sweep<0, true>(a, m, c, s, prm, st.refs, a.P[s], acc, sh.out, sh.red, TaylorSrc{}, nullptr,
+                   j0, j1, part + (size_t)c * ((a.nchan + 7) >> 3) * kScatPart);
+  (void)tid;
+}
+
+// The solver step of every running subint (one wave each).  ctrs: the
+// running counts by iteration parity -- this launch adds to ctrs[par] and
+// clears ctrs[par ^ 1] for the next one, so no memset runs between launches.
+__global__ __launch_bounds__(64) void k_scat_step(FitArgs a, const double* part, int init,
+                                                  int* ctrs, int par) {
+  __shared__ double out[kScatPart];
+  const int c = blockIdx.x;
+  if (c == 0 && threadIdx.x == 0) ctrs[par ^ 1] = 0;
+  if (!scat_split_owner(a, a.st[c])) return;
+  scat_step_wave(a, part, init, ctrs + par, out, c);
 }
 
 // ---------------------------------------------------------------------------

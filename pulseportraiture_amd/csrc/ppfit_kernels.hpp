@@ -738,7 +738,7 @@ __global__ void k_scat_taus(const double* freqs, int n, double tau, double alpha
 __global__ void k_guess(FitArgs a);
 constexpr int kScatPart = 24;  // split scattering sweep partial: f, g[5], H pairs[15], pad
 __global__ void k_scat_sweep(FitArgs a, double* part, int split, int init);
-__global__ void k_scat_step(FitArgs a, const double* part, int split, int init, int* active);
+__global__ void k_scat_step(FitArgs a, const double* part, int init, int* ctrs, int par);
 __global__ void k_model_mean(const double2* M, double2* Mmean, int nchan, int NHP);
 template <bool MOM>
 __global__ void k_fit_taylor(FitArgs a);
