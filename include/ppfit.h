@@ -16,6 +16,8 @@
  *                                                             pptoaslib.py:52-81
  *   ppf_rotate_accumulate   <- ppalign.align_archives' weighted sum
  *                              ppalign.py:202-208
+ *   ppf_rotate_accumulate_spec <- the same sum over cached data spectra
+ *                              (ppalign.py:202-208, iterations after the first)
  *   ppf_irfft_rows          <- numpy.fft.irfft (final step of ppalign.py:210-213)
  *   ppf_noise_rows          <- pplib.get_noise_PS(chans=True)  pplib.py:2227-2253
  *   ppf_unpack_subints      <- PSRCHIVE Archive_load + pscrunch in
@@ -176,6 +178,25 @@ int ppf_phase_profile(ppf_ctx* ctx, int32_t enable, uint64_t* out);
 #define PPF_SOLVE_EVAL 2
 #define PPF_GUESS_DIRECT 4
 
+/* Data-spectrum cache (spec_mode; ppalign's iterations, ppalign.py:160-213,
+ * refit the same subints against each new template).  The cache is the
+ * caller's: spec [nsub][nchan][NHP] complex (interleaved re, im; NHP =
+ * ppf_spec_nhp(nbin)), spec_sig and spec_dsum [nsub][nchan], spec_R
+ * [nsub][NHP] complex.
+ *   PPF_SPEC_STORE: the data pass also stores each subint's spectrum (rfft
+ *     of the row, DC included), noise sigma, sum |D|^2 / sigma^2 and guess
+ *     average in the cache (every other output as without the cache);
+ *   PPF_SPEC_USE: no data pass -- those come from the cache, and the Taylor
+ *     moment passes form the cross-spectrum D conj(M) from the cached
+ *     spectrum as they stream it: the same X, bitwise, so the same fits.
+ *     Only phase-family trust-ncg fits (tau = 0, not fitted; not
+ *     PPF_SOLVE_EXACT) take it, with the data, freqs, errs, mask, weights, P
+ *     and guess_nu of the STORE call.                                    */
+#define PPF_SPEC_NONE 0
+#define PPF_SPEC_STORE 1
+#define PPF_SPEC_USE 2
+int32_t ppf_spec_nhp(int32_t nbin);
+
 typedef struct {
   int32_t nsub, nchan, nbin, nmodel;
   int32_t fit_flags[5];   /* phi, DM, GM, tau, alpha (pptoaslib.py:928)     */
@@ -206,6 +227,11 @@ typedef struct {
   const double* bounds;     /* HOST pointer, [5][2] (low, high) per parameter
                                for the whole batch, NaN = None; read by
                                PPF_METHOD_TNC only (NULL = all None)        */
+  int32_t spec_mode;        /* PPF_SPEC_* (data-spectrum cache, above)       */
+  double* spec;             /* [nsub][nchan][NHP] complex, or NULL            */
+  double* spec_sig;         /* [nsub][nchan]                                  */
+  double* spec_dsum;        /* [nsub][nchan]                                  */
+  double* spec_R;           /* [nsub][NHP] complex                            */
 } ppf_fit_desc;
 
 typedef struct {
@@ -258,6 +284,12 @@ int ppf_rotate_rows(ppf_ctx* ctx, int32_t nrow, int32_t nbin, const double* in,
 int ppf_rotate_accumulate(ppf_ctx* ctx, int32_t nsub, int32_t nchan,
                           int32_t nbin, const double* data, const double* phase,
                           const double* weight, double* accum);
+/* The same sum from cached spectra (PPF_SPEC_STORE's spec, [nsub][nchan][NHP]
+ * complex): no FFT, one pass over the spectra.  Rows of channels the fit
+ * masked hold zeros (give them weight 0, as ppalign does).               */
+int ppf_rotate_accumulate_spec(ppf_ctx* ctx, int32_t nsub, int32_t nchan,
+                               int32_t nbin, const double* spec, const double* phase,
+                               const double* weight, double* accum);
 
 /* Gaussian-component template rows (gen_gaussian_portrait, pplib.py:853-930,
  * as read_model calls it, pplib.py:2873-2959): out[r][:] at freqs[r] for

@@ -23,6 +23,9 @@ KERNEL_IDS = {"model_fft": 0, "data_xspec": 1, "solve": 2, "phase_shift": 3,
 PPF_SOLVE_EXACT = 1
 PPF_SOLVE_EVAL = 2
 PPF_GUESS_DIRECT = 4
+PPF_SPEC_NONE = 0
+PPF_SPEC_STORE = 1
+PPF_SPEC_USE = 2
 PPF_SELFTEST_N = 10
 # ppf_set_option ids (include/ppfit.h)
 OPTIONS = {"scat_graph": 0, "scat_split": 1, "scat_tail": 2, "fuse_moments": 3, "guess_wave": 4}
@@ -44,7 +47,8 @@ class FitDesc(ctypes.Structure):
                 ("freqs", _dp), ("errs", _dp), ("chan_mask", _dp),
                 ("weights", _dp), ("P", _dp), ("init", _dp), ("nu_fit", _dp),
                 ("nu_out", _dp), ("guess_nu", _dp), ("guess_tau", _dp),
-                ("bounds", _dp)]
+                ("bounds", _dp), ("spec_mode", ctypes.c_int32), ("spec", _dp),
+                ("spec_sig", _dp), ("spec_dsum", _dp), ("spec_R", _dp)]
 
 
 class FitResult(ctypes.Structure):
@@ -87,6 +91,9 @@ EXPORTS = {
                          _dp], ctypes.c_int),
     "ppf_rotate_accumulate": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
                                ctypes.c_int32, _dp, _dp, _dp, _dp], ctypes.c_int),
+    "ppf_rotate_accumulate_spec": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                    ctypes.c_int32, _dp, _dp, _dp, _dp], ctypes.c_int),
+    "ppf_spec_nhp": ([ctypes.c_int32], ctypes.c_int32),
     "ppf_irfft_rows": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, _dp, _dp],
                        ctypes.c_int),
     "ppf_noise_rows": ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, _dp, _dp],

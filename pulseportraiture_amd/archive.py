@@ -57,7 +57,15 @@ class _Stack:
     each archive's bunch holding views of its own row, and ``rows`` one
     [narch, nsub, npol, nchan, nbin] view of their subints when those are
     equally spaced views of one tensor (else None).  allok: every archive's
-    ok_isubs is every subint and every ok_ichans every channel."""
+    ok_isubs is every subint and every ok_ichans every channel.  names /
+    bunches: the archives in registration order; views(): one read-only
+    _RegisteredView per archive, made once."""
+    _views = None
+
+    def views(self):
+        if self._views is None:
+            self._views = [_RegisteredView(b) for b in self.bunches]
+        return self._views
 
 
 def _stacked_view(subs):
@@ -104,6 +112,7 @@ def register_archives(names, bunches):
     nsub, npol, nchan, nbin = shape
     stk = _Stack()
     stk.nsub, stk.npol, stk.nchan, stk.nbin = shape
+    stk.names, stk.bunches = tuple(names), bs
     try:
         stk.freqs = np.stack([b.freqs for b in bs])
         stk.weights = np.stack([b.weights for b in bs])

@@ -250,11 +250,21 @@ size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
 // the first moment pass inside k_fit_taylor (default) or its own k_moments
 // launch (PPF_OPT_FUSE_MOMENTS = 0)
+// launch; the moment passes form X from the data-spectrum cache when fa.Dsp is set
 void launch_fit_taylor(const ppf_ctx* ctx, dim3 g, size_t lds, hipStream_t st, const FitArgs& fa) {
-  if (ctx->opt[PPF_OPT_FUSE_MOMENTS])
-    hipLaunchKernelGGL(k_fit_taylor<true>, g, dim3(kBlock), lds, st, fa);
-  else
-    hipLaunchKernelGGL(k_fit_taylor<false>, g, dim3(kBlock), lds, st, fa);
+  const bool mom = ctx->opt[PPF_OPT_FUSE_MOMENTS] != 0;
+  if (fa.Dsp) {
+    if (mom) hipLaunchKernelGGL((k_fit_taylor<true, true>), g, dim3(kBlock), lds, st, fa);
+    else hipLaunchKernelGGL((k_fit_taylor<false, true>), g, dim3(kBlock), lds, st, fa);
+  } else {
+    if (mom) hipLaunchKernelGGL((k_fit_taylor<true, false>), g, dim3(kBlock), lds, st, fa);
+    else hipLaunchKernelGGL((k_fit_taylor<false, false>), g, dim3(kBlock), lds, st, fa);
+  }
+}
+
+void launch_moments(dim3 g, hipStream_t st, const FitArgs& fa) {
+  if (fa.Dsp) hipLaunchKernelGGL((k_moments<4, true>), g, dim3(kBlock), 0, st, fa);
+  else hipLaunchKernelGGL((k_moments<4, false>), g, dim3(kBlock), 0, st, fa);
 }
 
 }  // namespace
@@ -413,6 +423,19 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   // fits, and every fit under PPF_SOLVE_EXACT, sweep it directly.
   const bool exact = (d->solver_flags & PPF_SOLVE_EXACT) != 0;
   const bool taylor = !exact && d->method == PPF_METHOD_TRUST_NCG;
+  // data-spectrum cache: sig, dsum and R live in the caller's arrays, and
+  // Taylor-path subints keep D instead of X (ppfit.h, PPF_SPEC_*)
+  const int smode = d->spec_mode;
+  if (smode != PPF_SPEC_NONE) {
+    if (smode != PPF_SPEC_STORE && smode != PPF_SPEC_USE)
+      return fail(ctx, PPF_ERR_INVALID, "spec_mode %d: PPF_SPEC_NONE, _STORE or _USE", smode);
+    if (!d->spec || !d->spec_sig || !d->spec_dsum || !d->spec_R)
+      return fail(ctx, PPF_ERR_INVALID, "spec_mode %d: spec, spec_sig, spec_dsum and spec_R "
+                  "are required", smode);
+    if (!taylor || d->fit_flags[3] || d->fit_flags[4])
+      return fail(ctx, PPF_ERR_UNSUPPORTED, "the data-spectrum cache takes phase-family "
+                  "trust-ncg fits only (tau and alpha not fitted, not PPF_SOLVE_EXACT)");
+  }
   // mean template spectrum for the unmasked guess
   double2* Mmean = nullptr;
   if (d->guess) {
@@ -468,6 +491,8 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   sa.log10_tau = d->log10_tau;
   sa.fit_tau = d->fit_flags[3] ? 1 : 0;
   sa.exact = exact ? 1 : 0;
+  sa.spec_mode = smode;
+  sa.D = nullptr;
   sa.X = reinterpret_cast<double2*>(base + offX);
   sa.R = reinterpret_cast<double2*>(base + offR);
   sa.sig = reinterpret_cast<double*>(base + offSig);
@@ -493,6 +518,7 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   for (int i = 0; i < 5; ++i)
     for (int j = 0; j < 2; ++j) fa.bounds[i][j] = d->bounds ? d->bounds[2 * i + j] : NAN;
   fa.X = sa.X;
+  fa.Dsp = nullptr;
   fa.R = sa.R;
   fa.M = M;
   fa.M2 = M2;
@@ -560,6 +586,19 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   }
   const size_t lds_guess =
       (size_t)(NHP + (d->guess ? pfa_scratch_slots(d->guess_Ns, NH) : 0)) * sizeof(double2);
+  // the cache rows of subints sub .. (spec_mode set): D, and sig / dsum / R in
+  // place of the workspace's
+  auto bind_spec = [&](SpecArgs& sp, FitArgs& fp, int64_t sub) {
+    if (smode == PPF_SPEC_NONE) return;
+    sp.D = reinterpret_cast<double2*>(d->spec) + (size_t)sub * nchan * NHP;
+    fp.Dsp = sp.D;
+    sp.sig = d->spec_sig + (size_t)sub * nchan;
+    fp.sig = sp.sig;
+    sp.dsum = d->spec_dsum + (size_t)sub * nchan;
+    fp.dsum = sp.dsum;
+    sp.R = reinterpret_cast<double2*>(d->spec_R) + (size_t)sub * NHP;
+    fp.R = sp.R;
+  };
   // Phase-family Taylor path, several pieces per chunk on two queues: piece
   // p's data pass starts when piece p-1's has finished, so the latency-bound
   // guess / fit / post-fit kernels of one piece run beside the HBM-bound
@@ -596,6 +635,7 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
         fp.T = fa.T + (size_t)off * 2 * nchan * kMT;
         fp.acc = fa.acc + (size_t)off * 2 * nchan * 10;
         fp.wsc = fa.wsc + (size_t)off * nchan * 8;
+        bind_spec(sp, fp, s0 + off);
         if (prev_x) HIPCHK(ctx, hipStreamWaitEvent(st, prev_x, 0));
         if (int r = timed_on(ctx, PPF_K_DATA_XSPEC, st, [&] {
               LOGN_SWITCH(logN, hipLaunchKernelGGL(k_data_xspec<LG>, dim3(n),
@@ -614,7 +654,7 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
         if (!ctx->opt[PPF_OPT_FUSE_MOMENTS])
           if (int r = timed_on(ctx, PPF_K_MOMENTS, st, [&] {
                 const dim3 g(n, (nchan + 16 * kWaves - 1) / (16 * kWaves));
-                hipLaunchKernelGGL(k_moments<4>, g, dim3(kBlock), 0, st, fp);
+                launch_moments(g, st, fp);
               }))
             return r;
         if (int r = timed_on(ctx, PPF_K_FIT_TAYLOR, st, [&] {
@@ -642,6 +682,7 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
     const int nc = (int)std::min<int64_t>(chunk, d->nsub - s0);
     sa.sub0 = (int)s0;
     fa.sub0 = (int)s0;
+    bind_spec(sa, fa, s0);
     if (int r = timed(ctx, PPF_K_DATA_XSPEC, [&] {
           LOGN_SWITCH(logN, hipLaunchKernelGGL(k_data_xspec<LG>, dim3(nc), dim3(XspecCfg<LG>::WPB * 64), xspec_dyn_lds(nchan),
                                                ctx->stream, sa));
@@ -774,7 +815,7 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
       if (!ctx->opt[PPF_OPT_FUSE_MOMENTS])
         if (int r = timed(ctx, PPF_K_MOMENTS, [&] {
               const dim3 g(nc, (nchan + 16 * kWaves - 1) / (16 * kWaves));
-              hipLaunchKernelGGL(k_moments<4>, g, dim3(kBlock), 0, ctx->stream, fa);
+              launch_moments(g, ctx->stream, fa);
             }))
           return r;
       if (int r = timed(ctx, PPF_K_FIT_TAYLOR, [&] {
@@ -1127,6 +1168,42 @@ int ppf_rotate_accumulate(ppf_ctx* ctx, int32_t nsub, int32_t nchan, int32_t nbi
           LOGN_SWITCH(logN, hipLaunchKernelGGL(k_rot_accum<LG>, dim3(nsplit * nchan),
                                                dim3(kBlock), 0, ctx->stream, data, phase, weight,
                                                partial, nsub, nchan, nsplit, tw));
+      }))
+    return r;
+  double2* acc = reinterpret_cast<double2*>(accum);
+  return timed(ctx, PPF_K_ROT_ACCUM, [&] {
+    hipLaunchKernelGGL(k_accum_reduce, dim3((unsigned)((count + 255) / 256)), dim3(256), 0,
+                       ctx->stream, partial, acc, nsplit, count);
+  });
+}
+
+int32_t ppf_spec_nhp(int32_t nbin) {
+  int logN;
+  if (check_nbin(nullptr, nbin, &logN)) return -1;
+  return nharm_pad(nbin);
+}
+
+int ppf_rotate_accumulate_spec(ppf_ctx* ctx, int32_t nsub, int32_t nchan, int32_t nbin,
+                               const double* spec, const double* phase, const double* weight,
+                               double* accum) {
+  if (!ctx || !spec || !phase || !weight || !accum)
+    return fail(ctx, PPF_ERR_INVALID, "null argument");
+  if (nsub <= 0 || nchan <= 0) return PPF_OK;
+  int logN;
+  if (int r = check_nbin(ctx, nbin, &logN)) return r;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  const int N = nbin / 2, NH = N + 1, NHP = nharm_pad(nbin);
+  // one workgroup per (slice, channel), about 2048 of them (8 per CU)
+  int nsplit = (2048 + nchan - 1) / nchan;
+  if (nsplit > nsub) nsplit = nsub;
+  if (nsplit < 1) nsplit = 1;
+  const size_t count = (size_t)nchan * NH;
+  if (int r = ensure(ctx, ctx->aux, (size_t)nsplit * count * sizeof(double2))) return r;
+  double2* partial = reinterpret_cast<double2*>(ctx->aux.p);
+  if (int r = timed(ctx, PPF_K_ROT_ACCUM, [&] {
+        hipLaunchKernelGGL(k_rot_accum_spec, dim3(nsplit * nchan), dim3(256), 0, ctx->stream,
+                           reinterpret_cast<const double2*>(spec), phase, weight, partial, nsub,
+                           nchan, nsplit, N, NHP);
       }))
     return r;
   double2* acc = reinterpret_cast<double2*>(accum);

@@ -10,7 +10,8 @@ namespace ppf {
 // ---------------------------------------------------------------------------
 struct SpecArgs {
   int sub0, nchan, NHP, kc, guess;
-  int log10_tau, fit_tau, exact;  // X is written only for subints that need it
+  int log10_tau, fit_tau, exact;  // which subints the Taylor path fits (spec_taylor_sub)
+  int spec_mode;           // PPF_SPEC_* (ppfit.h)
   const double* data;      // [nsub][nchan][nbin]
   const double2* M;        // [nmodel][nchan][NHP] DC-zeroed template spectra
   const int* model_idx;    // [nsub] or null
@@ -26,7 +27,16 @@ struct SpecArgs {
   double* sig;             // chunk [c][nchan]
   double* dsum;            // chunk [c][nchan]
   const double2* tw;
+  double2* D;              // chunk [c][nchan][NHP] data spectra (spec cache) or null
 };
+
+// Subint s fitted by the Taylor path (fused_taylor's test, on the data
+// pass's arguments): no scattering at the start and tau not fitted.
+__device__ __forceinline__ bool spec_taylor_sub(const SpecArgs& a, int s) {
+  const double t3 = a.init[(size_t)s * 5 + 3];
+  const double tl = a.log10_tau ? pow(10.0, t3) : t3;
+  return !a.exact && !a.fit_tau && tl == 0.0;
+}
 
 struct PhaseShiftArgs {
   int NHP, kc, Ns;
@@ -81,6 +91,8 @@ struct FitArgs {
   int method;                // PPF_METHOD_*
   int guess_wave;            // k_guess_w takes the subints it covers (guess_wave_ok)
   const double2* X;          // chunk [c][nchan][NHP]
+  const double2* Dsp;        // chunk [c][nchan][NHP] data spectra (spec cache): the
+                             // Taylor moment passes form X = D conj(M) from it
   const double2* R;          // chunk [c][NHP]
   const double2* M;          // [nmodel][nchan][NHP]
   const double* M2;          // [nmodel][nchan][NHP] |M|^2 (scattering sweeps)
@@ -723,6 +735,9 @@ __global__ void k_rot_accum(const double* data, const double* phase, const doubl
                             const double2* tw);
 __global__ void k_rot_accum_w(const double* data, const double* phase, const double* weight,
                               double2* partial, int nsub, int nchan, int nsplit, const double2* tw);
+__global__ void k_rot_accum_spec(const double2* spec, const double* phase, const double* weight,
+                                 double2* partial, int nsub, int nchan, int nsplit, int N,
+                                 int NHP);
 __global__ void k_accum_reduce(const double2* partial, double2* accum, int nsplit, size_t count);
 template <int LOGN> __global__ void k_resid_chi2(ResidArgs a, const double2* tw);
 __global__ void k_vpow(double2* vp, int N, int rows);
@@ -740,9 +755,9 @@ constexpr int kScatPart = 24;  // split scattering sweep partial: f, g[5], H pai
 __global__ void k_scat_sweep(FitArgs a, double* part, int split, int init);
 __global__ void k_scat_step(FitArgs a, const double* part, int init, int* ctrs, int par);
 __global__ void k_model_mean(const double2* M, double2* Mmean, int nchan, int NHP);
-template <bool MOM>
+template <bool MOM, bool DSP>
 __global__ void k_fit_taylor(FitArgs a);
-template <int U>
+template <int U, bool DSP>
 __global__ void k_moments(FitArgs a);
 __global__ void k_selftest(int* fails);
 template <bool SCAT> __global__ void k_solve(FitArgs a);

@@ -74,6 +74,11 @@ __global__ __launch_bounds__(kBlock) void k_model_spec(const double* __restrict_
 //   X[c][n][k]  = D_nk conj(M_nk)   only for subints fitted with the exact
 //                 (scattering) sweeps; phase-family subints get Taylor
 //                 moments from k_moments instead (ppfit_taylor.hip)
+// With the data-spectrum cache (a.D, PPF_SPEC_STORE) every row's spectrum
+// D_nk, k = 0 .. N, is stored as well, and Taylor-path subints write no X
+// (their moment passes form it from D).  PPF_SPEC_USE: those subints are not
+// visited at all (sig, dsum and R are the cached ones); the others are
+// processed as under STORE (the same values again) for their X.
 // Channels go in groups of WPB: wave w transforms channel g*WPB + w in its
 // own LDS buffer (wave-synchronous Stockham, next row already in registers)
 // and post-processes the spectrum in (k, N-k) pairs straight from the packed
@@ -125,6 +130,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
   uint8_t* cact = dyn + (size_t)a.nchan * sizeof(double2);  // fitted channel flags
   const int c = blockIdx.x;
   const int s = a.sub0 + c;
+  const bool tsub = a.D && spec_taylor_sub(a, s);
+  if (a.spec_mode == PPF_SPEC_USE && tsub) return;  // all of it cached
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: row pointers in SGPRs
   const int nchan = a.nchan;
@@ -165,7 +172,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
   }
   __syncthreads();
   const double wsum = s_meta[1];
-  const bool wx = a.X != nullptr;
+  const bool wx = a.X != nullptr && !tsub;
+  const bool wd = a.D != nullptr && a.spec_mode == PPF_SPEC_STORE;
   {
     const double nug = s_meta[0];
     const double Dfac = kDconst * s_meta[3] / a.P[s];
@@ -246,6 +254,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
         EN = turn_phasor((double)N, cm.x);
       }
       double2* Xr = wx ? a.X + ((size_t)c * nchan + n) * a.NHP : nullptr;
+      double2* Dr = wd ? a.D + ((size_t)c * nchan + n) * a.NHP : nullptr;
       double pn = 0.0, pd = 0.0;
       double2 tw = w0;
       // pair iteration i: k = lane + 64 i.  Every iteration but the last has
@@ -271,6 +280,10 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
           if (wx) {
             st_stream((k == 0) ? cmk(0.0, 0.0) : cmulc(xk, mk), Xr + k);
             if (two) st_stream(cmulc(xn, mn), Xr + kn);
+          }
+          if (wd) {
+            st_stream(xk, Dr + k);
+            if (two) st_stream(xn, Dr + kn);
           }
           if (a.guess) {
             // e^{2 pi i (N-k) phi} = e^{2 pi i N phi} conj(e^{2 pi i k phi});
@@ -300,7 +313,9 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
         pair(NPI - 1, std::false_type{}, m0k, m0n);
       }
       if (wx)
-      for (int k = NH + lane; k < a.NHP; k += 64) Xr[k] = cmk(0.0, 0.0);
+        for (int k = NH + lane; k < a.NHP; k += 64) Xr[k] = cmk(0.0, 0.0);
+      if (wd)
+        for (int k = NH + lane; k < a.NHP; k += 64) Dr[k] = cmk(0.0, 0.0);
       pn = wave_sum(pn);
       pd = wave_sum(pd);
       if (lane == 0) {
@@ -315,6 +330,10 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
       if (wx) {
         double2* Xr = a.X + ((size_t)c * nchan + n) * a.NHP;
         for (int k = lane; k < a.NHP; k += 64) Xr[k] = cmk(0.0, 0.0);
+      }
+      if (wd) {
+        double2* Dr = a.D + ((size_t)c * nchan + n) * a.NHP;
+        for (int k = lane; k < a.NHP; k += 64) Dr[k] = cmk(0.0, 0.0);
       }
     }
     if (a.guess) {
@@ -772,6 +791,60 @@ __global__ __launch_bounds__(256, 2) void k_rot_accum_w(const double* __restrict
     if (k <= N / 2) {
       out[k] = ak[i];
       if (k < N / 2) out[N - k] = an[i];  // k = 0: the Nyquist harmonic
+    }
+  }
+}
+
+// The same sum from cached data spectra (PPF_SPEC_STORE's spec, [nsub][nchan]
+// [NHP]): no transform, one streaming pass.  Workgroup (n, p) sums channel n
+// over subint slice p in subint order; thread t owns harmonics k = kb + t +
+// 256 i (i < kRotSpecK), with the row's rotation w e^{2 pi i k ph} from
+// turn_phasor at kb + t stepped by e^{2 pi i 256 ph}.  The next row's
+// harmonics load while this row's are added.  Rows of weight 0 add nothing.
+constexpr int kRotSpecK = 5;  // 1280 harmonics per pass: nbin <= 2048 in one
+__global__ __launch_bounds__(256) void k_rot_accum_spec(const double2* __restrict__ spec,
+                                                        const double* __restrict__ phase,
+                                                        const double* __restrict__ weight,
+                                                        double2* __restrict__ partial, int nsub,
+                                                        int nchan, int nsplit, int N, int NHP) {
+  const int tid = threadIdx.x;
+  const int n = blockIdx.x % nchan, p = blockIdx.x / nchan;
+  const int per = (nsub + nsplit - 1) / nsplit;
+  const int s0 = p * per, s1 = min(nsub, s0 + per);
+  double2* out = partial + ((size_t)p * nchan + n) * (N + 1);
+  for (int kb = 0; kb <= N; kb += 256 * kRotSpecK) {
+    double2 acc[kRotSpecK], cur[kRotSpecK], nxt[kRotSpecK] = {};
+    auto load = [&](int s, double2* v) {
+      const double2* r = spec + ((size_t)s * nchan + n) * NHP;
+#pragma unroll
+      for (int i = 0; i < kRotSpecK; ++i) {
+        const int k = kb + tid + 256 * i;
+        v[i] = r[k <= N ? k : N];  // clamped, unpredicated; k > N unused
+      }
+    };
+#pragma unroll
+    for (int i = 0; i < kRotSpecK; ++i) acc[i] = cmk(0.0, 0.0);
+    if (s0 < s1) load(s0, cur);
+    for (int s = s0; s < s1; ++s) {
+      const size_t row = (size_t)s * nchan + n;
+      const double w = weight[row], ph = phase[row];
+      if (s + 1 < s1) load(s + 1, nxt);
+      if (w != 0.0) {  // uniform per workgroup
+        const double2 st = turn_phasor(256.0, ph);
+        double2 e = cscale(turn_phasor((double)(kb + tid), ph), w);
+#pragma unroll
+        for (int i = 0; i < kRotSpecK; ++i) {
+          if (i > 0) e = cmul(e, st);
+          acc[i] = cadd(acc[i], cmul(cur[i], e));
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < kRotSpecK; ++i) cur[i] = nxt[i];
+    }
+#pragma unroll
+    for (int i = 0; i < kRotSpecK; ++i) {
+      const int k = kb + tid + 256 * i;
+      if (k <= N) out[k] = acc[i];
     }
   }
 }

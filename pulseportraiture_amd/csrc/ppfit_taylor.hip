@@ -121,7 +121,10 @@ __global__ void k_vpow(double2* vp, int N, int rows) {
 // restart from turn_phasor every kMomReseedSteps steps.  The next block's X and power rows
 // stream into each step's registers as soon as its MFMAs have issued, so U
 // steps of loads stay in flight with one register set.
-template <int U>
+// DSP (data-spectrum cache, a.Dsp): the lane loads D_k and M_k instead and
+// forms X_k = D_k conj(M_k) (0 at k = 0) -- k_data_xspec's arithmetic on the
+// same operands, so the same X bit for bit.
+template <int U, bool DSP>
 __device__ __forceinline__ void moment_tile16(const FitArgs& a, int c, int slot, int n, bool ok,
                                               double phic) {
   static_assert(kMT == 32, "two 16-row MFMA tiles");
@@ -131,7 +134,14 @@ __device__ __forceinline__ void moment_tile16(const FitArgs& a, int c, int slot,
   const int N = a.nbin / 2;
   const int nblk = ((N + 1 + 3) / 4 + U - 1) / U;  // blocks of U 4-harmonic steps
   const int col = lane & 15, kk = lane >> 4;
-  const double2* __restrict__ Xr = a.X + ((size_t)c * a.nchan + (ok ? n : 0)) * a.NHP;
+  const size_t xrow = ((size_t)c * a.nchan + (ok ? n : 0)) * a.NHP;
+  const double2* __restrict__ Xr = (DSP ? a.Dsp : a.X) + xrow;
+  const double2* __restrict__ Mr = nullptr;
+  if constexpr (DSP) {
+    const int s = a.sub0 + c;
+    const int midx = a.model_idx ? a.model_idx[s] : 0;
+    Mr = a.M + ((size_t)midx * a.nchan + (ok ? n : 0)) * a.NHP;
+  }
   // power row of step t for this lane: vpow[(4 t + kk) * 16 + col]
   const double2* __restrict__ vp = a.vpow + (size_t)kk * 16 + col;
   const double2 s8 = turn_phasor(8.0, phic);
@@ -140,14 +150,22 @@ __device__ __forceinline__ void moment_tile16(const FitArgs& a, int c, int slot,
   f64x4 g0 = d0, g1 = d0, g2 = d0, g3 = d0;
   // loads are unpredicated (X index clamped to N; the power table is padded
   // past the last block); cells k > N and idle lanes are zeroed at use
-  double2 xb[U], pb[U];
+  double2 xb[U], pb[U], mb[DSP ? U : 1];
 #pragma unroll
   for (int t = 0; t < U; ++t) {
     xb[t] = xload(Xr + min(4 * t + kk, N));
+    if constexpr (DSP) mb[t] = Mr[min(4 * t + kk, N)];
     pb[t] = vp[(size_t)t * 64];
   }
-  auto xcell = [&](int t, const double2& x) {
-    return (ok && 4 * t + kk <= N) ? x : cmk(0.0, 0.0);
+  // step t's cell from register set i
+  auto xcell = [&](int t, int i) {
+    const int k = 4 * t + kk;
+    if constexpr (DSP) {
+      const double2 x = cmulc(xb[i], mb[i]);
+      return (ok && k >= 1 && k <= N) ? x : cmk(0.0, 0.0);
+    } else {
+      return (ok && k <= N) ? xb[i] : cmk(0.0, 0.0);
+    }
   };
   double2 e0 = cmk(1.0, 0.0), e1 = e0;
   for (int b = 0; b < nblk; ++b) {
@@ -157,8 +175,8 @@ __device__ __forceinline__ void moment_tile16(const FitArgs& a, int c, int slot,
     }
 #pragma unroll
     for (int u = 0; u < UP; ++u) {
-      const double2 W0 = cmul(xcell(b * U + 2 * u, xb[2 * u]), e0);
-      const double2 W1 = cmul(xcell(b * U + 2 * u + 1, xb[2 * u + 1]), e1);
+      const double2 W0 = cmul(xcell(b * U + 2 * u, 2 * u), e0);
+      const double2 W1 = cmul(xcell(b * U + 2 * u + 1, 2 * u + 1), e1);
       const double2 p0 = pb[2 * u], p1 = pb[2 * u + 1];
       d0 = __builtin_amdgcn_mfma_f64_16x16x4f64(p0.x, W0.x, d0, 0, 0, 0);
       d1 = __builtin_amdgcn_mfma_f64_16x16x4f64(p0.y, W0.x, d1, 0, 0, 0);
@@ -175,6 +193,7 @@ __device__ __forceinline__ void moment_tile16(const FitArgs& a, int c, int slot,
       for (int h = 0; h < 2; ++h) {
         const int t = 2 * u + h;
         xb[t] = xload(Xr + min(4 * ((b + 1) * U + t) + kk, N));
+        if constexpr (DSP) mb[t] = Mr[min(4 * ((b + 1) * U + t) + kk, N)];
         pb[t] = vp[(size_t)((b + 1) * U + t) * 64];
       }
     }
@@ -201,8 +220,8 @@ __device__ __forceinline__ void moment_tile16(const FitArgs& a, int c, int slot,
 // chain (the p chain of moment_tile16), keeps the part it feeds to B and
 // trades the other with its partner (DPP quad_perm [1,0,3,2]).  Powers are
 // formed inline in the table's order, and every MFMA sees the operands of
-// moment_tile16: bitwise the same moments.
-template <int U>
+// moment_tile16: bitwise the same moments.  DSP: as moment_tile16's.
+template <int U, bool DSP>
 __device__ __forceinline__ void moment_tile8(const FitArgs& a, int c, int slot, int n, bool ok,
                                              double phic) {
   static_assert(kMT == 32, "two 16-row MFMA tiles");
@@ -212,7 +231,19 @@ __device__ __forceinline__ void moment_tile8(const FitArgs& a, int c, int slot, 
   const int N = a.nbin / 2;
   const int nblk = ((N + 1 + 3) / 4 + U - 1) / U;
   const int col = lane & 15, part = col & 1, kk = lane >> 4;
-  const double2* __restrict__ Xr = a.X + ((size_t)c * a.nchan + (ok ? n : 0)) * a.NHP;
+  const size_t xrow = ((size_t)c * a.nchan + (ok ? n : 0)) * a.NHP;
+  const double2* __restrict__ Xr = (DSP ? a.Dsp : a.X) + xrow;
+  const double2* __restrict__ Mr = nullptr;
+  if constexpr (DSP) {
+    const int s = a.sub0 + c;
+    const int midx = a.model_idx ? a.model_idx[s] : 0;
+    Mr = a.M + ((size_t)midx * a.nchan + (ok ? n : 0)) * a.NHP;
+  }
+  // X_k of this lane (0 for k past N and idle lanes)
+  auto xget = [&](bool on, int k) {
+    if constexpr (DSP) return (on && k >= 1 && k <= N) ? cmulc(Xr[k], Mr[k]) : cmk(0.0, 0.0);
+    else return (on && k <= N) ? Xr[k] : cmk(0.0, 0.0);
+  };
   const double2 s8 = turn_phasor(8.0, phic);
   const double iN = 1.0 / (double)N;
   f64x4 d0 = {0.0, 0.0, 0.0, 0.0}, d1 = d0, d2 = d0, d3 = d0;
@@ -220,7 +251,7 @@ __device__ __forceinline__ void moment_tile8(const FitArgs& a, int c, int slot, 
 #pragma unroll
   for (int u = 0; u < UP; ++u) {
     const int k = 4 * (2 * u + part) + kk;
-    xb[u] = (ok && k <= N) ? Xr[k] : cmk(0.0, 0.0);
+    xb[u] = xget(ok, k);
   }
   double2 e = cmk(1.0, 0.0);
   for (int b = 0; b < nblk; ++b) {
@@ -240,7 +271,7 @@ __device__ __forceinline__ void moment_tile8(const FitArgs& a, int c, int slot, 
       d3 = __builtin_amdgcn_mfma_f64_16x16x4f64(p1.y, bv1, d3, 0, 0, 0);
       e = cmul(e, s8);
       const int k = 4 * ((b + 1) * U + 2 * u + part) + kk;
-      xb[u] = (more && ok && k <= N) ? Xr[k] : cmk(0.0, 0.0);
+      xb[u] = xget(more && ok, k);
     }
   }
   d0 += d2;
@@ -257,6 +288,7 @@ __device__ __forceinline__ void moment_tile8(const FitArgs& a, int c, int slot, 
 }
 
 // All fitted channels of subint c, all threads of the block (recentring).
+template <bool DSP>
 __device__ void moments_from_X(const FitArgs& a, const Meta& m, int c, int s, int slot,
                                const double* xc, const double* refs, double P) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -264,7 +296,7 @@ __device__ void moments_from_X(const FitArgs& a, const Meta& m, int c, int s, in
   for (int t = w; t * 8 < m.nok; t += kWaves) {
     const int j = t * 8 + chl;
     const bool ok = j < m.nok;
-    moment_tile8<8>(a, c, slot, ok ? m.chan[j] : 0, ok,
+    moment_tile8<DSP ? 4 : 8, DSP>(a, c, slot, ok ? m.chan[j] : 0, ok,
                     ok ? phase_frac(xc, m.fr[j], refs, P) : 0.0);
   }
 }
@@ -275,7 +307,7 @@ __device__ void moments_from_X(const FitArgs& a, const Meta& m, int c, int s, in
 // full occupancy.  Block (c, y): wave w takes channels 16 (4 y + w) .. + 15
 // (masked channels idle in their lane).
 // ---------------------------------------------------------------------------
-template <int U>
+template <int U, bool DSP>
 __global__ __launch_bounds__(kBlock, 3) void k_moments(FitArgs a) {
   const int c = blockIdx.x, s = a.sub0 + c;
   if (!fused_taylor(a, s)) return;
@@ -287,10 +319,11 @@ __global__ __launch_bounds__(kBlock, 3) void k_moments(FitArgs a) {
   const bool ok = n < a.nchan && (!a.mask || a.mask[(size_t)s * a.nchan + n]);
   const double phic = ok ? phase_frac(st.xc[0], a.freqs[(size_t)s * a.nchan + n], st.refs, a.P[s])
                          : 0.0;
-  moment_tile16<U>(a, c, 0, n, ok, phic);
+  moment_tile16<U, DSP>(a, c, 0, n, ok, phic);
 }
 
-template __global__ void k_moments<4>(FitArgs);
+template __global__ void k_moments<4, false>(FitArgs);
+template __global__ void k_moments<4, true>(FitArgs);
 
 // ---------------------------------------------------------------------------
 // k_fit_taylor: one workgroup per phase-family subint, the whole fit:
@@ -357,7 +390,7 @@ __device__ __forceinline__ double wave_reach(const Meta& m, double p0, double p1
 // one subint with the latency-bound trust-region iterations of another
 // (measured: 9.26 -> 9.03 ms per headline step; fusing the post-fit too
 // spilled 784 B per lane and was slower, 10.0 ms).
-template <bool MOM>
+template <bool MOM, bool DSP>
 __global__ __launch_bounds__(kBlock, 3) void k_fit_taylor(FitArgs a) {
   extern __shared__ __align__(16) unsigned char dyn[];
   __shared__ TaylorShared sh;
@@ -385,7 +418,7 @@ __global__ __launch_bounds__(kBlock, 3) void k_fit_taylor(FitArgs a) {
       const bool ok = n < a.nchan && (!a.mask || a.mask[(size_t)s * a.nchan + n]);
       const double phic =
           ok ? phase_frac(st0.xc[0], a.freqs[(size_t)s * a.nchan + n], st0.refs, a.P[s]) : 0.0;
-      moment_tile16<4>(a, c, 0, n, ok, phic);
+      moment_tile16<DSP ? 2 : 4, DSP>(a, c, 0, n, ok, phic);
     }
     // T slot 0 is read back below by other waves of this workgroup
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -491,7 +524,7 @@ __global__ __launch_bounds__(kBlock, 3) void k_fit_taylor(FitArgs a) {
     }
     if (tid < 5) sh.xc[wsl][tid] = p[tid];
     __syncthreads();
-    moments_from_X(a, m, c, s, wsl, sh.xc[wsl], refs, P);
+    moments_from_X<DSP>(a, m, c, s, wsl, sh.xc[wsl], refs, P);
     __syncthreads();
     if (wsl == 0 && tl) stage_T0(a, c, tl);
     if (tid == 0) {
@@ -617,8 +650,10 @@ __global__ __launch_bounds__(kBlock, 3) void k_fit_taylor(FitArgs a) {
   }
 }
 
-template __global__ void k_fit_taylor<false>(FitArgs);
-template __global__ void k_fit_taylor<true>(FitArgs);
+template __global__ void k_fit_taylor<false, false>(FitArgs);
+template __global__ void k_fit_taylor<true, false>(FitArgs);
+template __global__ void k_fit_taylor<false, true>(FitArgs);
+template __global__ void k_fit_taylor<true, true>(FitArgs);
 
 // ---------------------------------------------------------------------------
 // Device self-test of the cross-lane primitives (DPP, permlane swaps,

@@ -312,7 +312,7 @@ class Engine:
                   model_idx=None, log10_tau=False, option=0, is_toa=True,
                   guess=False, guess_Ns=100, guess_wrap=True, guess_nu=None,
                   guess_tau=None, exact=False, method="trust-ncg", bounds=None,
-                  eval_only=False, guess_direct=False):
+                  eval_only=False, guess_direct=False, spec_cache=None):
         """fit_portrait_full over a batch (pptoaslib.py:928-1096).
 
         data [nsub, nchan, nbin]; model [nmodel, nchan, nbin] (or [nchan, nbin]);
@@ -325,6 +325,11 @@ class Engine:
         bounds: 5 (low, high) pairs, None = unbounded (TNC only).
         eval_only: f, g, H and the post-fit at init, no solver step.
         guess_direct: brute-force guess grid by direct sums (no folded DFT).
+        spec_cache: a SpecCache (Engine.spec_cache) for refits of the same
+        subints against new templates (ppalign's iterations): its first fit
+        stores the data spectra, later ones skip the data pass (ppfit.h,
+        PPF_SPEC_*).  Phase-family trust-ncg fits only, with every input but
+        the model the same as the first call's.
         Returns a dict of device tensors ("errs": the per-channel noise sigma
         each channel was fitted with, 0 for masked channels).
         """
@@ -391,6 +396,15 @@ class Engine:
         desc.weights, desc.P, desc.init = _ptr(wt), _ptr(Pt), _ptr(it)
         desc.nu_fit, desc.nu_out = _ptr(nf), _ptr(no)
         desc.guess_nu, desc.guess_tau = _ptr(gn), _ptr(gt)
+        if spec_cache is not None:
+            sc = spec_cache
+            if (sc.nsub, sc.nchan, sc.nbin) != (nsub, nchan, nbin):
+                raise PPFitError("spec_cache is for %s, data %s" % (
+                    (sc.nsub, sc.nchan, sc.nbin), (nsub, nchan, nbin)))
+            desc.spec_mode = _lib.PPF_SPEC_USE if sc.stored else _lib.PPF_SPEC_STORE
+            desc.spec, desc.spec_sig = _ptr(sc.spec), _ptr(sc.sig)
+            desc.spec_dsum, desc.spec_R = _ptr(sc.dsum), _ptr(sc.R)
+            keep["spec"] = sc
         out = _result_tensors(nsub, nchan, dev)
         res = _lib.FitResult()
         for k in ["params", "param_errs", "nu_out", "cov", "scales", "scale_errs",
@@ -400,6 +414,8 @@ class Engine:
         res.errs_out = _ptr(out["errs"])
         self._chk(self.lib.ppf_fit_portrait_batch(self.ctx, ctypes.byref(desc),
                                                   ctypes.byref(res)))
+        if spec_cache is not None:
+            spec_cache.stored = True
         out["_keep"] = keep  # inputs must outlive the stream-ordered call
         return out
 
@@ -733,6 +749,27 @@ class Engine:
                                                  _ptr(w), _ptr(accum)))
         return (d, ph, w)
 
+    def spec_cache(self, nsub, nchan, nbin):
+        """An empty data-spectrum cache for fit_batch(spec_cache=...) and
+        rotate_accumulate_spec: nsub * nchan * NHP complex spectra (NHP =
+        ppf_spec_nhp(nbin)) plus per-row sigma / sum |D|^2 and per-subint
+        guess averages, on this engine's device."""
+        return SpecCache(self, nsub, nchan, nbin)
+
+    def rotate_accumulate_spec(self, cache, phase, weight, accum):
+        """rotate_accumulate over the cached data spectra of a stored
+        SpecCache (no transform): accum [nchan, nharm, 2] += weighted rotated
+        spectra."""
+        if not cache.stored:
+            raise PPFitError("rotate_accumulate_spec: the cache holds no spectra yet")
+        dev = self.device
+        n, nchan, nbin = cache.nsub, cache.nchan, cache.nbin
+        ph = _dev_f64(phase, dev).reshape(n, nchan).contiguous()
+        w = _dev_f64(weight, dev).reshape(n, nchan).contiguous()
+        self._chk(self.lib.ppf_rotate_accumulate_spec(self.ctx, n, nchan, nbin, _ptr(cache.spec),
+                                                      _ptr(ph), _ptr(w), _ptr(accum)))
+        return (cache, ph, w)
+
     def synth(self, model, phase, sigma, seed, sub0=0, out=None):
         """Synthetic portraits [nsub, nchan, nbin] on device (pplib.py:3342-3377 math)."""
         dev = self.device
@@ -869,6 +906,28 @@ class FitPipeline:
     def collect(self):
         tag, out, ph = self.pending.popleft()
         return tag, ph.wait()
+
+
+class SpecCache:
+    """Device arrays of the data-spectrum cache (ppfit.h, PPF_SPEC_*):
+    spec [nsub, nchan, NHP, 2], sig / dsum [nsub, nchan], R [nsub, NHP, 2].
+    stored: a fit has filled it (later fits read it)."""
+
+    def __init__(self, eng, nsub, nchan, nbin):
+        nhp = int(eng.lib.ppf_spec_nhp(int(nbin)))
+        if nhp <= 0:
+            raise PPFitError("nbin=%d: must be a power of two in [64, 8192]" % nbin)
+        f64 = dict(dtype=torch.float64, device=eng.device)
+        self.nsub, self.nchan, self.nbin, self.nhp = int(nsub), int(nchan), int(nbin), nhp
+        self.spec = torch.empty((nsub, nchan, nhp, 2), **f64)
+        self.sig = torch.empty((nsub, nchan), **f64)
+        self.dsum = torch.empty((nsub, nchan), **f64)
+        self.R = torch.empty((nsub, nhp, 2), **f64)
+        self.stored = False
+
+    @property
+    def nbytes(self):
+        return sum(t.numel() * 8 for t in (self.spec, self.sig, self.dsum, self.R))
 
 
 def get_engine(device=None):

@@ -10,6 +10,8 @@ spectrum and the channel weights per iteration -- RCCL over xGMI with the
 "nccl" backend.  Every rank then divides locally and holds the new template.
 """
 import gc
+import itertools
+import operator
 
 import numpy as np
 import torch
@@ -18,6 +20,13 @@ from . import archive as _arch
 from .pplib import (DataBunch, Dconst, guess_fit_freq, gaussian_profile, rotate_data,
                     fit_phase_shift)
 from .pptoaslib import fit_portraits_batch
+
+# Keep every unit's data spectrum on the device after the first iteration's
+# data pass (Engine.spec_cache): later iterations refit from it without
+# transforming the data again, and the rotate-and-sum reads it instead of
+# the time-domain rows.  Needs about the data's size again in HBM; off, or
+# without the room, every iteration transforms the data twice as before.
+SPEC_CACHE = True
 
 rm_baseline = False
 
@@ -50,6 +59,39 @@ def allreduce_sum(*tensors):
     return tensors
 
 
+class _StackOpened(list):
+    """_open_all's result when it is one register_archives stack, whole and
+    in order (``stk``): _Bulk reads the stack without visiting the archives."""
+    stk = None
+
+
+def _open_stack(datafiles, reg, nbin, SNR_cutoff):
+    """_open_all for exactly the archives of one register_archives stack, in
+    registration order, each still registered as it was and passing the nbin
+    and S/N checks: the checks as C-level maps over the bunches (their
+    current values) instead of a Python visit per archive.  None when that
+    does not apply (the per-archive path then runs, with its messages)."""
+    if not reg or not datafiles or not isinstance(datafiles[0], str):
+        return None
+    b0 = reg.get(datafiles[0])
+    s = b0.get("_stack") if b0 is not None else None
+    if s is None or s[1] != 0:
+        return None
+    stk = s[0]
+    bs = stk.bunches
+    n = len(bs)
+    if len(datafiles) != n or tuple(datafiles) != stk.names or \
+            not all(map(operator.is_, map(reg.get, stk.names), bs)):
+        return None
+    nb = np.fromiter(map(operator.itemgetter("nbin"), bs), dtype=np.int64, count=n)
+    snr = np.fromiter(map(operator.itemgetter("prof_SNR"), bs), dtype=np.float64, count=n)
+    if (nb != nbin).any() or (snr < SNR_cutoff).any():
+        return None
+    out = _StackOpened(zip(stk.names, stk.views()))
+    out.stk = stk
+    return out
+
+
 def _open_all(datafiles, model_data, SNR_cutoff, quiet, skip_these, tscrunch, pscrunch):
     """Metadata of every archive (ppalign.py:121-159's checks, no DATA read):
     [(name, Archive)] of the archives to align."""
@@ -59,6 +101,9 @@ def _open_all(datafiles, model_data, SNR_cutoff, quiet, skip_these, tscrunch, ps
     reg = _arch._registry if not tscrunch and not rm_baseline else {}
     RV = _arch._RegisteredView
     nbin = model_data.nbin
+    fast = _open_stack(datafiles, reg, nbin, SNR_cutoff)
+    if fast is not None:
+        return fast
     for name in datafiles:
         b = reg.get(name) if isinstance(name, str) else None
         if b is not None:
@@ -179,22 +224,29 @@ class _Bulk:
     def _from_stack(opened, mfq, nchan):
         """build() for archives of one archive.register_archives stack, opened
         as registered views: slices (or one fancy index) of the stack."""
-        RV = _arch._RegisteredView
-        if not all(type(a) is RV for _, a in opened):
-            return None
-        st = [a.meta.get("_stack") for _, a in opened]
-        s0 = st[0]
-        if s0 is None:
-            return None
-        stk = s0[0]
-        if not all(s is not None and s[0] is stk for s in st) or stk.nchan != nchan:
-            return None
-        idx = np.fromiter((s[1] for s in st), dtype=np.int64, count=len(st))
-        n = len(idx)
-        if n == 1 or (np.diff(idx) == 1).all():
-            sel = slice(int(idx[0]), int(idx[0]) + n)
+        if isinstance(opened, _StackOpened):  # the whole stack, in order
+            stk = opened.stk
+            if stk.nchan != nchan:
+                return None
+            n = len(opened)
+            sel = slice(0, n)
         else:
-            sel = idx
+            RV = _arch._RegisteredView
+            if not all(type(a) is RV for _, a in opened):
+                return None
+            st = [a.meta.get("_stack") for _, a in opened]
+            s0 = st[0]
+            if s0 is None:
+                return None
+            stk = s0[0]
+            if not all(s is not None and s[0] is stk for s in st) or stk.nchan != nchan:
+                return None
+            idx = np.fromiter((s[1] for s in st), dtype=np.int64, count=len(st))
+            n = len(idx)
+            if n == 1 or (np.diff(idx) == 1).all():
+                sel = slice(int(idx[0]), int(idx[0]) + n)
+            else:
+                sel = idx
         nsub = stk.nsub
         R = n * nsub
         b = _Bulk()
@@ -221,8 +273,9 @@ class _Bulk:
             # a device gather of every selected archive's subints on every
             # rank; they take the per-archive rows instead
             b.rows_view = stk.rows[sel].reshape(R, nchan, stk.nbin)
-        b.regs = [a.meta.subints for _, a in opened]
-        b.index = {name: i for i, (name, _) in enumerate(opened)}
+        b.regs = list(map(operator.itemgetter("subints"), stk.bunches)) \
+            if isinstance(opened, _StackOpened) else [a.meta.subints for _, a in opened]
+        b.index = dict(zip(map(operator.itemgetter(0), opened), range(n)))
         b.nsub = nsub
         return b
 
@@ -242,7 +295,12 @@ def _units(opened, model_data, bulk=None):
         # one register_archives stack, every channel on everywhere: every
         # subint a unit with the shared ALL, in bulk row order
         ns = bulk.nsub
-        units = [(name, isub, ALL, ALL) for name, _ in opened for isub in range(ns)]
+        if ns == 1:
+            names = map(operator.itemgetter(0), opened)
+            units = list(zip(names, itertools.repeat(0), itertools.repeat(ALL),
+                             itertools.repeat(ALL)))
+        else:
+            units = [(name, isub, ALL, ALL) for name, _ in opened for isub in range(ns)]
         bulk.unit_rows = np.arange(len(units), dtype=np.int64)
         return units
     if bulk is not None:
@@ -307,8 +365,15 @@ def _guess_fit_freq_rows(freqs, snrs):
     is the one guess_fit_freq(freqs[i], snrs[i]) returns."""
     f = np.ascontiguousarray(freqs, dtype=np.float64)
     w = np.ascontiguousarray(snrs, dtype=np.float64)
-    if len(f) > 1 and (f == f[0]).all() and (w == w[0]).all():  # one distinct row
-        return np.full(len(f), guess_fit_freq(f[0], w[0]))
+    if len(f) > 1 and (f == f[0]).all():
+        if (w == w[0]).all():  # one distinct row
+            return np.full(len(f), guess_fit_freq(f[0], w[0]))
+        # one frequency row: its terms once, broadcast (the same elementwise
+        # operations on the same values, so the same sums)
+        f0 = f[0]
+        nu0 = (f0.min() + f0.max()) * 0.5
+        f2 = f0 ** -2
+        return nu0 + np.sum((f0 - nu0) * w * f2, axis=1) / np.sum(w * f2, axis=1)
     nu0 = (f.min(axis=1) + f.max(axis=1)) * 0.5
     f2 = f ** -2
     return nu0 + np.sum((f - nu0[:, None]) * w * f2, axis=1) / np.sum(w * f2, axis=1)
@@ -520,6 +585,24 @@ class _UnitStack:
         self.nu_fit = _guess_fit_freq_rows(freqs, bulk.S[rows])
         return True
 
+    def _spec_cache(self, eng):
+        """The units' data-spectrum cache (SPEC_CACHE), made on first use
+        when it fits in free device memory with a quarter to spare; None
+        otherwise."""
+        sc = getattr(self, "_spec", False)
+        if sc is not False:
+            return sc
+        sc = None
+        d = self.pols[0]
+        if SPEC_CACHE and isinstance(d, torch.Tensor) and d.device.type == "cuda":
+            n, nchan, nbin = d.shape
+            need = (n * nchan * (nbin // 2 + 9) + n * (nbin // 2 + 9)) * 16 + 2 * n * nchan * 8
+            free, _ = torch.cuda.mem_get_info(d.device)
+            if need < 0.75 * free:
+                sc = eng.spec_cache(n, nchan, nbin)
+        self._spec = sc
+        return sc
+
     def fit_and_accumulate(self, eng, model_port, fit_dm, accum, tw, mark=None):
         """One iteration's fits (ppalign.py:178-195) and weighted rotate-and-sum
         (ppalign.py:202-208) in the Fourier domain.  The fit results stay on
@@ -544,11 +627,12 @@ class _UnitStack:
                             nu=torch.as_tensor(self.nu_fit, **f64))
         dv = self._dv
         flags = [1, int(bool(fit_dm)), 0, 0, 0]
+        spec = self._spec_cache(eng)
         out = fit_portraits_batch(self.pols[0], model_port, dv["init"], dv["P"], dv["freqs"],
                                   nu_fits=dv["nu3"], errs=dv["errs"], fit_flags=flags,
                                   log10_tau=False, chan_mask=dv["mask"], weights=dv["wts"],
                                   guess=True, guess_Ns=model_port.shape[1], guess_wrap=False,
-                                  guess_nu=dv["nu"], to_host=False)
+                                  guess_nu=dv["nu"], to_host=False, spec_cache=spec)
         if mark is not None:
             t0 = mark("fit", t0)
         out = {k: torch.as_tensor(out[k], device=dev) for k in ("params", "nu_out", "scales",
@@ -562,7 +646,10 @@ class _UnitStack:
         w = torch.where(dv["on"], out["scales"] / e2, torch.zeros((), dtype=torch.float64,
                                                                  device=dev))
         for ipol, pol in enumerate(self.pols):
-            eng.rotate_accumulate(pol, ph, w, accum[ipol])
+            if ipol == 0 and spec is not None:  # the fitted polarisation's cached spectra
+                eng.rotate_accumulate_spec(spec, ph, w, accum[0])
+            else:
+                eng.rotate_accumulate(pol, ph, w, accum[ipol])
         tw += w.sum(dim=0).to(tw.device)
         if mark is not None:
             mark("accumulate", t0)
@@ -634,7 +721,7 @@ def align_archives(metafile, initial_guess, fit_dm=True, tscrunch=False, pscrunc
             gc.enable()
     t0 = mark("unit_stack", t0)
     archives = {}
-    for name, a in opened:  # 1-channel hack units (rare): their archives on the host
+    for name, a in (opened if single else ()):  # 1-channel hack units (rare): on the host
         if any(u[0] == name for u in single):
             archives[name] = _arch.load_data(name, dedisperse=False, tscrunch=tscrunch,
                                              pscrunch=pscrunch, rm_baseline=rm_baseline,

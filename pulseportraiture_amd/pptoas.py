@@ -272,8 +272,10 @@ class GetTOAs:
         (archive, subint) units in get_TOAs order are split into contiguous
         shards, one per rank of an initialised torch.distributed group, and a
         rank reads only the subint range of its shard (pptoas.py:246,343 is the
-        loop being sharded).  Fits run in one device call per archive and flag
-        set.  Every rank turns its own shard's results into columns -- the
+        loop being sharded).  Fits are submitted per archive and flag set, a
+        large one in pieces (``pipeline_fracs``), through ``fit_pipeline``
+        (engine.FitPipeline): the device fits piece i + 1 while the host turns
+        piece i's results into records and text.  Every rank turns its own shard's results into columns -- the
         per-subint arrays and a TOABlock of its TOA records, with the .tim text
         already formatted when there is more than one rank -- and only those
         finished columns travel: to rank 0 (``gather_to`` "root", default),

@@ -87,13 +87,14 @@ def fit_portraits_batch(data, model, init, P, freqs, nu_fits=None, nu_outs=None,
                         is_toa=True, chan_mask=None, weights=None, model_idx=None,
                         guess=False, guess_Ns=100, guess_wrap=True, guess_nu=None,
                         guess_tau=None, method="trust-ncg", bounds=None, device=None,
-                        to_host=True, host_keys=None):
+                        to_host=True, host_keys=None, spec_cache=None):
     """Batched fit_portrait_full over subints; returns arrays keyed like its DataBunch.
 
     method selects the device solver as minimize(method=...) does in the
     reference (pptoaslib.py:995-1014); bounds are applied by TNC only.
     host_keys: the result keys to copy to the host (None: all) -- one
-    packed D2H (engine.results_to_host)."""
+    packed D2H (engine.results_to_host).  spec_cache: Engine.fit_batch's
+    data-spectrum cache (device-resident data only)."""
     if method not in ("trust-ncg", "TNC", "Newton-CG", "TNC-legacy"):
         print("Method '%s' is not implemented." % method)
         sys.exit()
@@ -112,10 +113,14 @@ def fit_portraits_batch(data, model, init, P, freqs, nu_fits=None, nu_outs=None,
         # host-resident subints: chunks staged through pinned buffers and
         # copied to the device on a second stream while the previous chunk is
         # fitted (Engine.fit_batch_streamed)
+        if spec_cache is not None:
+            raise ValueError("spec_cache: device-resident data only")
         per = int(np.prod(np.shape(data)[1:])) * 8
         out = eng.fit_batch_streamed(data, model, freqs, P, init, fit_flags,
                                      chunk=max(1, STREAM_CHUNK_BYTES // per), **kw)
     else:
+        if spec_cache is not None:
+            kw["spec_cache"] = spec_cache
         out = eng.fit_batch(data, model, freqs, P, init, fit_flags, **kw)
     if not to_host:
         return out

@@ -7,7 +7,8 @@ from tests.conftest import ROOT
 
 def header_symbols():
     txt = open(os.path.join(ROOT, "include", "ppfit.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(ppf_\w+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int32_t|void|const char\*)\s+(ppf_\w+)\s*\(", txt,
+                                 re.M)))
 
 
 def test_header_declares_entry_points():

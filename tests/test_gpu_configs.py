@@ -144,6 +144,17 @@ def test_align_archives_config5_shape(gpu):
         if niter == 2:
             ref = z["aligned_niter2_f32"].astype(np.float64)
             np.testing.assert_allclose(port, ref, atol=2e-6 * np.abs(ref).max())
+            # without the data-spectrum cache (every iteration transforms the
+            # data again): the same portrait to rounding (the rotate-and-sum
+            # forms the spectra with other twiddles)
+            assert ppalign.SPEC_CACHE
+            ppalign.SPEC_CACHE = False
+            try:
+                plain = ppalign.align_archives(names, "guess5.fits", fit_dm=True, niter=niter,
+                                               quiet=True)[0]
+            finally:
+                ppalign.SPEC_CACHE = True
+            np.testing.assert_allclose(port, plain, rtol=0, atol=1e-11 * np.abs(plain).max())
 
 
 def test_headline_2000_subints_vs_reference(gpu):

@@ -147,3 +147,51 @@ def test_register_archives_mixed_shapes_register_each():
     finally:
         for nm in names + ["mx_guess"]:
             archive.unregister_archive(nm)
+
+
+def test_open_stack_fast_path():
+    """_open_all on exactly one register_archives stack, in order, takes the
+    stack path (_StackOpened: no per-archive visit) and opens the same
+    archives as the per-archive loop; any other request declines it."""
+    rng = np.random.default_rng(11)
+    n = 5
+    names = ["os_%d" % i for i in range(n)]
+    bs = _bunches(n, "plain", rng)
+    archive.register_archives(names, bs)
+    archive.register_archive("os_guess", dict(subints=np.zeros((1, 1, NCHAN, NBIN)), freqs=FREQS,
+                                              Ps=[0.004], epochs=[(57000, 0, 0.0)], DM=10.0,
+                                              dmc=1))
+    model = archive.load_data("os_guess", dedisperse=True, tscrunch=True, rm_baseline=True,
+                              quiet=True)
+
+    def opened(nms, cutoff=0.0):
+        skip = []
+        o = ppalign._open_all(nms, model, cutoff, True, skip, False, True)
+        return o, skip
+
+    try:
+        o, skip = opened(names)
+        assert isinstance(o, ppalign._StackOpened) and not skip
+        assert [nm for nm, _ in o] == names
+        assert all(a.meta is archive._registry[nm] for nm, a in o)
+        # declined: another order, a subset, an S/N cut that skips one
+        for nms in (names[::-1], names[:3]):
+            o2, _ = opened(nms)
+            assert not isinstance(o2, ppalign._StackOpened)
+            assert [nm for nm, _ in o2] == nms
+        archive._registry[names[2]]["prof_SNR"] = 1.0
+        o3, skip = opened(names, cutoff=5.0)
+        assert not isinstance(o3, ppalign._StackOpened) and skip == [names[2]]
+        assert [nm for nm, _ in o3] == names[:2] + names[3:]
+        archive._registry[names[2]]["prof_SNR"] = np.inf
+        # one archive registered again on its own: not the stack any more
+        archive.register_archive(names[1], dict(bs[1]))
+        o4, _ = opened(names)
+        assert not isinstance(o4, ppalign._StackOpened)
+        assert o4[1][1].meta is archive._registry[names[1]]
+        archive.unregister_archive(names[3])
+        o5, skip = opened(names)
+        assert not isinstance(o5, ppalign._StackOpened) and names[3] not in [nm for nm, _ in o5]
+    finally:
+        for nm in names + ["os_guess"]:
+            archive.unregister_archive(nm)
