@@ -684,10 +684,13 @@ def main_gm_shard(args, eng, rank, world):
     input -- more than HBM), fitted phase+DM+GM in chunks.  Inside the timed
     region each chunk is generated on the device (k_synth: template, injected
     phi / DM, Philox noise -- what reading the archives would put in HBM),
-    fitted, and its per-TOA results copied to pinned host memory; HIP events
-    split generation from fitting.  Beside it, the same run times the
-    2,000-subint slice (--config gm's step) to compare per-TOA rates, and
-    samples subints across the shard against the oracle."""
+    fitted, and its per-TOA results copied to pinned host memory.  Chunk
+    i + 1 is generated into the other of two buffers on a second queue (its
+    own libppfit context) while chunk i is fitted -- the way a reader would
+    fill the next chunk during the fits; HIP events time each side.  Beside
+    it, the same run times the 2,000-subint slice (--config gm's step) to
+    compare per-TOA rates, and samples subints across the shard against the
+    oracle."""
     import torch
     from pulseportraiture_amd import synth, pplib
     nsub0, nchan, nbin, flags, _, _, _, desc = CONFIGS["gm_shard"]
@@ -701,9 +704,16 @@ def main_gm_shard(args, eng, rank, world):
     freqs = torch.as_tensor(w0.freqs, device=dev)
     starts = list(range(0, N, C))
     # chunk metadata (injected phases per channel) on the host before timing
-    phases = [synth.make_workload(min(C, N - s0), nchan, nbin, seed=args.seed,
-                                  sub0=base + s0).phase for s0 in starts]
-    buf = torch.empty((C, nchan, nbin), dtype=torch.float64, device=dev)
+    phases = [torch.as_tensor(synth.make_workload(min(C, N - s0), nchan, nbin, seed=args.seed,
+                                                  sub0=base + s0).phase, device=dev)
+              for s0 in starts]
+    bufs = [torch.empty((C, nchan, nbin), dtype=torch.float64, device=dev)
+            for _ in range(2 if len(starts) > 1 else 1)]
+    buf = bufs[0]
+    from pulseportraiture_amd.engine import Engine
+    gstream = torch.cuda.Stream(dev)
+    geng = Engine(dev.index)  # the generator's own context, on its own queue
+    geng.bind_stream(gstream)
     P = torch.full((C,), w0.P, dtype=torch.float64, device=dev)
     init = torch.tensor([[0.0, w0.DM0, 0.0, 0.0, 0.0]] * C, dtype=torch.float64, device=dev)
     nu = torch.full((C, 3), nu_fit, dtype=torch.float64, device=dev)
@@ -715,29 +725,54 @@ def main_gm_shard(args, eng, rank, world):
     S = max(0, args.cpu_sample) if world == 1 else 0
     samp = np.sort(rng.choice(N, size=min(S, N), replace=False)) if S else np.zeros(0, int)
     pport = torch.empty((max(len(samp), 1), nchan, nbin), dtype=torch.float64, pin_memory=True)
-    stream = torch.cuda.current_stream()
+    stream = eng.stream
     ev = []
 
     def run(record):
+        nb = len(bufs)
+        gen = [None] * len(starts)   # (start, end) events of each chunk's generation
+        done = [None] * len(starts)  # each chunk's fit (and sample copies) finished
+
+        def generate(ci):
+            s0 = starts[ci]
+            n = min(C, N - s0)
+            if ci >= nb:  # the buffer's previous chunk fitted
+                gstream.wait_event(done[ci - nb])
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(gstream)
+            geng.synth(w0.template, phases[ci], w0.sigma, args.seed, sub0=base + s0,
+                       out=bufs[ci % nb][:n])
+            b.record(gstream)
+            gen[ci] = (a, b)
+
+        generate(0)
         for ci, s0 in enumerate(starts):
             n = min(C, N - s0)
-            e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
-            e0.record(stream)
-            eng.synth(w0.template, phases[ci], w0.sigma, args.seed, sub0=base + s0, out=buf[:n])
+            b = bufs[ci % nb]
+            if ci + 1 < len(starts):
+                generate(ci + 1)
+            stream.wait_event(gen[ci][1])
+            e1, e2 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e1.record(stream)
-            out = eng.fit_batch(buf[:n], model, freqs, P[:n], init[:n], flags, nu_fit=nu[:n],
+            out = eng.fit_batch(b[:n], model, freqs, P[:n], init[:n], flags, nu_fit=nu[:n],
                                 guess=True, guess_Ns=100)
             e2.record(stream)
-            for k in small:
-                host[k][s0:s0 + n].copy_(out[k], non_blocking=True)
+            with torch.cuda.stream(stream):
+                for k in small:
+                    host[k][s0:s0 + n].copy_(out[k], non_blocking=True)
+                if record:
+                    for j in np.flatnonzero((samp >= s0) & (samp < s0 + n)):
+                        pport[j].copy_(b[int(samp[j]) - s0], non_blocking=True)
+            d = torch.cuda.Event()
+            d.record(stream)
+            done[ci] = d
             if record:
-                ev.append((e0, e1, e2))
-                for j in np.flatnonzero((samp >= s0) & (samp < s0 + n)):
-                    pport[j].copy_(buf[int(samp[j]) - s0], non_blocking=True)
+                ev.append((gen[ci][0], gen[ci][1], e1, e2))
         torch.cuda.synchronize()
 
     # warm-up: one chunk (workspace and allocator at steady size)
-    eng.synth(w0.template, phases[0], w0.sigma, args.seed, sub0=base, out=buf[:min(C, N)])
+    geng.synth(w0.template, phases[0], w0.sigma, args.seed, sub0=base, out=buf[:min(C, N)])
+    torch.cuda.synchronize()
     eng.fit_batch(buf[:min(C, N)], model, freqs, P[:min(C, N)], init[:min(C, N)], flags,
                   nu_fit=nu[:min(C, N)], guess=True, guess_Ns=100)
     torch.cuda.synchronize()
@@ -750,8 +785,8 @@ def main_gm_shard(args, eng, rank, world):
         torch.distributed.barrier()
     t1 = time.perf_counter()
     elapsed, rank_times = dist_times(t1 - t0, world, dev)
-    gen_ms = sum(a.elapsed_time(b) for a, b, _ in ev)
-    fit_ms = sum(b.elapsed_time(c) for _, b, c in ev)
+    gen_ms = sum(a.elapsed_time(b) for a, b, _, _ in ev)
+    fit_ms = sum(c.elapsed_time(d) for _, _, c, d in ev)
     status = host["status"].numpy()
     nfev = host["nfev"].numpy()
     # the 2,000-subint slice (--config gm's step) in the same process
@@ -769,7 +804,8 @@ def main_gm_shard(args, eng, rank, world):
         sstep()
     torch.cuda.synchronize()
     slice_ms = (time.perf_counter() - ts0) / 10 * 1e3
-    del dS
+    del dS, bufs, buf
+    geng.close()
     if rank != 0:
         if world > 1:
             torch.distributed.destroy_process_group()
@@ -801,6 +837,8 @@ def main_gm_shard(args, eng, rank, world):
                    "input_gb_per_gpu": round(N * nchan * nbin * 8 / 1e9, 1),
                    "parallelism": "subint-sharded dp%d" % world},
         "generate_ms": round(gen_ms, 2), "fit_ms": round(fit_ms, 2),
+        "overlap": "chunk i + 1 generated on a second queue while chunk i is fitted "
+                   "(two buffers); generate_ms / fit_ms are each side's own event time",
         "fit_only_value": round(N / (fit_ms / 1e3), 2),
         "per_toa_us": round(per_toa_us, 4), "fit_only_per_toa_us": round(fit_ms * 1e3 / N, 4),
         "slice_2000": {"ms_per_step": round(slice_ms, 3),

@@ -61,7 +61,10 @@ __host__ __device__ constexpr int kVpowRows(int N) { return N + 1 + 4 * 64; }
 constexpr int kMTerm = kMT - 2;
 // largest LDS copy of one T slot k_fit_taylor keeps (48 KB: nchan <= 96), so
 // that two of its blocks (the register limit) still fit a CU's 160 KB of LDS
-constexpr size_t kTaylorLds = 48 * 1024;
+#ifndef PPF_TAYLOR_LDS_KB
+#define PPF_TAYLOR_LDS_KB 48
+#endif
+constexpr size_t kTaylorLds = PPF_TAYLOR_LDS_KB * 1024;
 constexpr double kTaylorY = 3.0;
 
 // Per-subint solver state handed from k_guess -> k_solve -> k_post (global).

@@ -469,9 +469,15 @@ __global__ __launch_bounds__(kBlock) void k_phase_shift(PhaseShiftArgs a) {
 // Row rotation: out = irfft(rfft(in) e^{2 pi i k phase}) (rotate_data),
 // optionally scattered: / (1 + 2 pi i k tau) (scattering_portrait_FT).
 // ---------------------------------------------------------------------------
-template <int LOGN>
+// epi(j, v): the value stored at complex sample j (bins 2j, 2j + 1), given
+// the transform's v -- a fused epilogue (k_synth adds its noise there)
+struct C2rPlain {
+  __device__ double2 operator()(int, double2 v) const { return v; }
+};
+template <int LOGN, typename Epi = C2rPlain>
 __device__ void c2r_from_spectrum(double2* buf, double2 (&xs)[((1 << LOGN) + kBlock) / kBlock + 1],
-                                  const double2* __restrict__ tw, double* __restrict__ out) {
+                                  const double2* __restrict__ tw, double* __restrict__ out,
+                                  Epi epi = Epi()) {
   constexpr int N = 1 << LOGN;
   constexpr int KI = (N + 1 + kBlock - 1) / kBlock;
   const int tid = threadIdx.x;
@@ -502,7 +508,7 @@ __device__ void c2r_from_spectrum(double2* buf, double2 (&xs)[((1 << LOGN) + kBl
   lds_fft<LOGN, true>(buf, tw);
   const double inv = 1.0 / (double)N;
   double2* o2 = reinterpret_cast<double2*>(out);
-  for (int j = tid; j < N; j += kBlock) o2[j] = cscale(buf[j], inv);
+  for (int j = tid; j < N; j += kBlock) o2[j] = epi(j, cscale(buf[j], inv));
 }
 
 template <int LOGN>
@@ -618,24 +624,21 @@ __global__ __launch_bounds__(kBlock) void k_synth(const double2* __restrict__ Mf
     if (k <= N) xs[i] = cmul(Mfull[(size_t)n * NHP + k], turn_phasor((double)k, ph));
   }
   double* out = data + (size_t)row * 2 * N;
-  c2r_from_spectrum<LOGN>(buf, xs, tw, out);
-  __syncthreads();
-  if (sigma != 0.0) {
-    double2* o2 = reinterpret_cast<double2*>(out);
-    const uint64_t gs = (uint64_t)(s + sub0);
-    for (int j = threadIdx.x; j < N; j += kBlock) {
+  // the noise joins each sample pair as it is stored (one pass over the row)
+  const uint64_t gs = (uint64_t)(s + sub0);
+  c2r_from_spectrum<LOGN>(buf, xs, tw, out, [&](int j, double2 v) {
+    if (sigma != 0.0) {
       u32x4 ctr;
       ctr.v[0] = (uint32_t)j;
       ctr.v[1] = (uint32_t)n;
       ctr.v[2] = (uint32_t)gs;
       ctr.v[3] = (uint32_t)(gs >> 32);
       const double2 z = philox_normal2(ctr, seed);
-      double2 v = o2[j];
       v.x = fma(sigma, z.x, v.x);
       v.y = fma(sigma, z.y, v.y);
-      o2[j] = v;
     }
-  }
+    return v;
+  });
 }
 
 // ---------------------------------------------------------------------------

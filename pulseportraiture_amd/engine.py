@@ -5,6 +5,7 @@ HIP stream handle.  All numerics run in the HIP kernels of libppfit.so.
 """
 import collections
 import ctypes
+import functools
 
 import numpy as np
 import torch
@@ -786,6 +787,30 @@ class Engine:
         out._keep = (m, ph)
         return out
 
+
+def _on_engine_stream(fn):
+    """Run an Engine call with its stream current: the temporaries it makes
+    (device copies of host arguments, outputs) are then allocated for the
+    stream its kernels run on, so the caching allocator cannot hand their
+    memory to other work while those kernels may still use it (an engine
+    bound to a side stream, e.g. a second context generating data beside the
+    fits).  A no-op when the engine's stream is already current."""
+    @functools.wraps(fn)
+    def run(self, *args, **kw):
+        if torch.cuda.current_stream(self.device) == self.stream:
+            return fn(self, *args, **kw)
+        with torch.cuda.stream(self.stream):
+            return fn(self, *args, **kw)
+    return run
+
+
+for _name in ("fit_batch", "phase_shift_batch", "rotate_rows", "gaussian_portraits",
+              "spline_portraits", "instrumental_response_rows", "response_table", "tscrunch",
+              "remove_baseline", "profile_snr", "irfft_rows", "noise_rows", "resid_chi2_rows",
+              "scatter_rotate_rows", "rotate_accumulate", "spec_cache", "rotate_accumulate_spec",
+              "synth"):
+    setattr(Engine, _name, _on_engine_stream(getattr(Engine, _name)))
+del _name
 
 _engines = {}
 
