@@ -68,26 +68,36 @@ PMC_TRAFFIC = {c: os.path.join(ROOT, "profiles", "%s_pmc_traffic_%s.json" % (r, 
                             ("ppalign", "r04e"))}
 KERNEL_SYMBOL = {"solve": "k_scat_sweep", "data_xspec": "k_data_xspec<10>",
                  "rot_accum": "k_rot_accum_w",
-                 "post": "k_post<false>", "guess": "k_guess_w", "moments": "k_moments<4>",
-                 "fit_taylor": "k_fit_taylor<true>"}
+                 "post": "k_post<false>", "guess": "k_guess_w", "moments": "k_moments<4, false>",
+                 "fit_taylor": "k_fit_taylor<true, false>"}
+# ppalign with the data-spectrum cache (ppalign.SPEC_CACHE): the rotate-and-sum
+# and the fit read the cached spectra
+KERNEL_SYMBOL_PPALIGN = dict(KERNEL_SYMBOL, rot_accum="k_rot_accum_spec",
+                             fit_taylor="k_fit_taylor<false, true>", guess="k_guess")
+# align_archives calls in one `bench.py --config ppalign` run (warm-up, two
+# timed, one with kernel timing): PMC bytes per call = all launches / this
+PPALIGN_CALLS = 4
 # fp64 operations of one scattering cell evaluation as cells_scat forms them
 # (ppfit_fit.hip: phasor step 6, W 6, B 13, f 8, g1 9, three conjugate
 # products 18, ten accumulations 30; the hardware reciprocal not counted)
 SCAT_FLOPS_PER_CELL = 90.0
 
 
-def pmc_traffic(kernel, nsub, config, per_step=False):
+def pmc_traffic(kernel, nsub, config, per_step=False, per_call=False):
     """Counter-measured HBM bytes per subint x nsub for this config, else None.
     per_step: all the kernel's launches of the PMC run (one step, bench
     --steps 1 --warmup 0) scaled to nsub, for kernels launched many times a
-    step."""
+    step.  per_call (ppalign): all launches / PPALIGN_CALLS, scaled."""
     f = PMC_TRAFFIC.get(config)
     if f is None or not os.path.exists(f):
         return None
     rec = json.load(open(f))
-    k = rec["kernels"].get(KERNEL_SYMBOL.get(kernel, ""))
+    sym = (KERNEL_SYMBOL_PPALIGN if config == "ppalign" else KERNEL_SYMBOL).get(kernel, "")
+    k = rec["kernels"].get(sym)
     if k is None:
         return None
+    if per_call:
+        return k["bytes_all_launches"] / PPALIGN_CALLS * nsub / rec["nsub"]
     if per_step:
         return k["bytes_all_launches"] * nsub / rec["nsub"] if "bytes_all_launches" in k else None
     return k["bytes_per_subint"] * nsub
@@ -933,7 +943,7 @@ def main_ppalign(args, eng, rank, world):
         # the call (rot_accum's timed launches also count its small partial-
         # sum reduction; data_xspec's later-iteration launches under the
         # cache visit the non-Taylor subints only, none here)
-        tr = pmc_traffic(k, narch, "ppalign")
+        tr = pmc_traffic(k, narch, "ppalign", per_call=True) if cache else None
         secs = ms / 1e3
         kernels[k] = {"bound": "hbm", "achieved": round(b / secs / 1e9, 1), "peak": HBM_PEAK_GBS,
                       "unit": "GB/s", "frac": round(b / secs / 1e9 / HBM_PEAK_GBS, 4),
@@ -944,7 +954,7 @@ def main_ppalign(args, eng, rank, world):
     roof = None
     if dom:
         roof = dict(kernel=dom, **kernels[dom])
-        roof["traffic_unit"] = "bytes/launch"
+        roof["traffic_unit"] = "HBM bytes per align_archives call (PMC run, all launches / calls)"
         src = PMC_TRAFFIC["ppalign"]
         roof["traffic_source"] = os.path.relpath(src, ROOT) if roof["traffic"] else None
         roof["other_kernels"] = {k: v for k, v in kernels.items() if k != dom}
