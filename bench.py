@@ -64,8 +64,8 @@ FP64_PEAK_TFLOPS = 78.6  # AMD MI355X spec, fp64 vector = fp64 matrix (not in th
 # HBM bytes per launch per kernel from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
 # passes over this same bench (tools/profile_r03.sh + tools/pmc_summary.py)
 PMC_TRAFFIC = {c: os.path.join(ROOT, "profiles", "%s_pmc_traffic_%s.json" % (r, c))
-               for c, r in (("headline", "r04g"), ("scattering", "r04c"), ("gm", "r04c"),
-                            ("ppalign", "r04e"))}
+               for c, r in (("headline", "r05"), ("scattering", "r05"), ("gm", "r05"),
+                            ("ppalign", "r05"))}
 KERNEL_SYMBOL = {"solve": "k_scat_sweep", "data_xspec": "k_data_xspec<10>",
                  "rot_accum": "k_rot_accum_w",
                  "post": "k_post<false>", "guess": "k_guess_w", "moments": "k_moments<4, false>",
@@ -449,18 +449,15 @@ def main():
     w, data, kw, tau_g = synth_inputs(eng, fit_config, nsub, args.seed, rank * nsub)
     torch.cuda.synchronize()
     small = ["params", "param_errs", "nu_out", "red_chi2", "snr", "status", "nfev"]
-    pinned = {}
+    from pulseportraiture_amd.engine import results_to_host
 
     def step():
         out = eng.fit_batch(data, kw["model"], kw["freqs"], kw["P"], kw["init"], flags,
                             nu_fit=kw["nu"], log10_tau=log10_tau, guess=True, guess_Ns=100,
                             guess_tau=kw["gtau"])
-        for k in small:
-            if k not in pinned:
-                pinned[k] = torch.empty(out[k].shape, dtype=out[k].dtype, pin_memory=True)
-            pinned[k].copy_(out[k], non_blocking=True)
-        torch.cuda.current_stream().synchronize()
-        return out, pinned
+        # the per-TOA results on the host: one D2H of the packed span that
+        # holds them (plus nfev / status), waited for
+        return out, results_to_host(out, small, eng.stream)
 
     if config == "get_toas":
         return main_get_toas(args, eng, rank, world, w, data, step, desc)
@@ -491,7 +488,6 @@ def main():
         for name in ["data_xspec", "guess", "moments", "fit_taylor", "solve", "post", "model_fft"]:
             ktimes[name] = eng.kernel_time(name)
         eng.set_timing(False)
-    host = {k: v.numpy().copy() for k, v in host.items()}
     status, nfev = host["status"], host["nfev"]
 
     # ---- PCIe-inclusive rate (config gm): the same subints from pinned host
@@ -873,7 +869,6 @@ def main_get_toas(args, eng, rank, world, w, data, step, desc):
     steps = max(1, args.steps)
     g, gt = leg_get_toas(eng, w, data, reps=steps)
     out, host = step()
-    host = {k: v.numpy().copy() for k, v in host.items()}
     same = float(np.max(np.abs(np.asarray(gt.phis[0]) - host["params"][:, 0]) /
                         host["param_errs"][:, 0]))
     gh, _ = leg_get_toas(eng, w, data, reps=1, host=True)

@@ -155,26 +155,41 @@ _TORCH_DT = {"<f8": torch.float64, "|u1": torch.uint8, "<i4": torch.int32}
 
 # fit results: float64 keys and their widths per subint ("c" = nchan), in
 # the order of one packed device buffer -- the keys the drivers read first,
-# so their host copy is one contiguous prefix (fit_portraits_batch)
-RESULT_F64 = [("params", (5,)), ("param_errs", (5,)), ("nu_out", (3,)), ("cov", (5, 5)),
-              ("scales", "c"), ("scale_errs", "c"), ("channel_snrs", "c"), ("chi2", ()),
-              ("red_chi2", ()), ("snr", ()), ("init_used", (5,)), ("fun", ()),
+# so their host copy is one contiguous prefix: the per-TOA scalars (params
+# .. snr) then get_TOAs' per-channel keys (through channel_snrs)
+RESULT_F64 = [("params", (5,)), ("param_errs", (5,)), ("nu_out", (3,)), ("chi2", ()),
+              ("red_chi2", ()), ("snr", ()), ("cov", (5, 5)), ("scales", "c"),
+              ("scale_errs", "c"), ("channel_snrs", "c"), ("init_used", (5,)), ("fun", ()),
               ("cov_nosc", (5, 5)), ("grad", (5,)), ("hess", (5, 5)), ("errs", "c")]
+_LAYOUTS = {}
+
+
+def _layout(nsub, nchan):
+    """(key, offset, shape, size) of every float64 result and the total, for
+    one (nsub, nchan) (cached: a batch loop asks for the same one each call)."""
+    lay = _LAYOUTS.get((nsub, nchan))
+    if lay is None:
+        rows, o = [], 0
+        for k, w in RESULT_F64:
+            sh = (nsub, nchan) if w == "c" else (nsub,) + w
+            n = int(np.prod(sh))
+            rows.append((k, o, sh, n))
+            o += n
+        if len(_LAYOUTS) > 64:
+            _LAYOUTS.clear()
+        lay = _LAYOUTS[(nsub, nchan)] = (rows, o)
+    return lay
 
 
 def _result_tensors(nsub, nchan, dev):
     """Result tensors of one fit call as views of one float64 buffer (and
     nfev / status of one int32 buffer); "_packed" holds (buffer, int32
     buffer, layout)."""
-    shapes = [(k, (nsub, nchan) if w == "c" else (nsub,) + w) for k, w in RESULT_F64]
-    sizes = [int(np.prod(sh)) for _, sh in shapes]
-    flat = torch.empty(sum(sizes), dtype=torch.float64, device=dev)
+    rows, total = _layout(nsub, nchan)
+    flat = torch.empty(total, dtype=torch.float64, device=dev)
     iflat = torch.empty(2 * nsub, dtype=torch.int32, device=dev)
-    out, lay, o = {}, [], 0
-    for (k, sh), n in zip(shapes, sizes):
-        out[k] = flat[o:o + n].view(sh)
-        lay.append((k, o, sh))
-        o += n
+    out = {k: flat[o:o + n].view(sh) for k, o, sh, n in rows}
+    lay = [(k, o, sh) for k, o, sh, _ in rows]
     out["nfev"], out["status"] = iflat[:nsub], iflat[nsub:]
     out["_packed"] = (flat, iflat, lay)  # not a tensor: key loops over tensors skip it
     return out
