@@ -275,14 +275,14 @@ class GetTOAs:
         loop being sharded).  Fits are submitted per archive and flag set, a
         large one in pieces (``pipeline_fracs``), through ``fit_pipeline``
         (engine.FitPipeline): the device fits piece i + 1 while the host turns
-        piece i's results into records and text.  Every rank turns its own shard's results into columns -- the
-        per-subint arrays and a TOABlock of its TOA records, with the .tim text
-        already formatted when there is more than one rank -- and only those
-        finished columns travel: to rank 0 (``gather_to`` "root", default),
-        which concatenates them in unit order into the per-archive lists and
-        TOA_list, or to every rank ("all").  With "root" the other ranks add
-        nothing to their lists (their shard's blocks stay in
-        ``shard_blocks``)."""
+        piece i's results into records and text.  Every rank turns its own
+        shard's results into columns -- the per-subint arrays and a TOABlock
+        of its TOA records, with the .tim text already formatted when there
+        is more than one rank -- and only those finished columns travel: to
+        rank 0 (``gather_to`` "root", default), which concatenates them in
+        unit order into the per-archive lists and TOA_list, or to every rank
+        ("all").  With "root" the other ranks add nothing to their lists
+        (their shard's blocks stay in ``shard_blocks``)."""
         if quiet is None:
             quiet = self.quiet
         warning = "You are using an experimental functionality of pptoas!"

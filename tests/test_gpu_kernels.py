@@ -165,3 +165,35 @@ def test_rotate_accumulate(eng, nsub, nchan, nbin):
     ref = np.sum(w[..., None] * np.fft.rfft(data, axis=-1) *
                  np.exp(2j * np.pi * ph[..., None] * k), axis=0)
     np.testing.assert_allclose(got, ref, atol=1e-11 * np.abs(ref).max())
+
+
+def test_engine_on_side_stream_keeps_its_temporaries(eng):
+    """An engine bound to a side stream (a second context generating data
+    beside the fits, bench --config gm_shard) allocates its temporaries for
+    that stream: host arguments dropped right after the call cannot be
+    reused by other work while its kernel still reads them.  The default
+    stream is kept busy meanwhile; every chunk must equal the same synth on
+    the default stream."""
+    import torch
+    from pulseportraiture_amd import synth
+    from pulseportraiture_amd.engine import Engine
+    w = synth.make_workload(64, 32, 1024, seed=77)
+    side = torch.cuda.Stream(eng.device)
+    geng = Engine(eng.device.index)
+    geng.bind_stream(side)
+    try:
+        ref = [eng.synth(w.template, w.phase * (1 + i), w.sigma, 5, sub0=64 * i) for i in range(4)]
+        torch.cuda.synchronize()
+        outs = [torch.empty_like(ref[0]) for _ in range(4)]
+        busy = torch.randn(4096, 4096, dtype=torch.float64, device=eng.device)
+        for i in range(4):
+            for _ in range(3):  # the default stream is busy (and allocates)
+                busy = busy @ busy.T / 4096.0
+            geng.synth(w.template, w.phase * (1 + i), w.sigma, 5, sub0=64 * i, out=outs[i])
+            scratch = torch.full((1 << 20,), float(i), device=eng.device)  # reuse bait
+            del scratch
+        torch.cuda.synchronize()
+        for r, o in zip(ref, outs):
+            assert torch.equal(r, o)
+    finally:
+        geng.close()
