@@ -888,9 +888,17 @@ class GetTOAs:
         alla = bool(allok.all()) if dense else bool(allok[ok_isubs].all())
         if alla and uniform_freqs and (snr == snr[0]).all():
             return np.full(len(ok_isubs), guess_fit_freq(f[0], snr[0]))  # one distinct row
-        nu0 = (f.min(axis=1) + f.max(axis=1)) * 0.5
-        f2 = f ** -2
-        out = nu0 + np.sum((f - nu0[:, None]) * snr * f2, axis=1) / np.sum(snr * f2, axis=1)
+        if uniform_freqs:
+            # one frequency row: its terms once, broadcast over the S/N rows
+            # (the same elementwise operations on the same values)
+            f0 = np.asarray(f[0], dtype=np.float64)
+            nu0 = (f0.min() + f0.max()) * 0.5
+            f2 = f0 ** -2
+            out = nu0 + np.sum((f0 - nu0) * snr * f2, axis=1) / np.sum(snr * f2, axis=1)
+        else:
+            nu0 = (f.min(axis=1) + f.max(axis=1)) * 0.5
+            f2 = f ** -2
+            out = nu0 + np.sum((f - nu0[:, None]) * snr * f2, axis=1) / np.sum(snr * f2, axis=1)
         for j in np.flatnonzero(~allok[ok_isubs]):
             isub = ok_isubs[j]
             ok = wn[isub]
