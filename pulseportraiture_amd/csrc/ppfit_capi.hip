@@ -575,6 +575,8 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   const bool split_scat = ctx->opt[PPF_OPT_SCAT_SPLIT] && d->fit_flags[3] &&
                           d->method == PPF_METHOD_TRUST_NCG;
   const int split = std::max(1, std::min(16, nchan / 64));
+  // the two-phase sweep's rows (any block's channel range at split or more)
+  const size_t lds_scat = PPF_SCAT_TWO_PHASE ? scat_sweep_lds(nchan, split) : lds_meta;
   if (split_scat) {
     if (int r = ensure(ctx, ctx->spart,
                        (size_t)chunk * ((nchan + 7) / 8) * kScatPart * sizeof(double) +
@@ -745,7 +747,7 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
         hipGraph_t g = nullptr;
         HIPCHK(ctx, hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
         for (int k = 0; k < kCheck; ++k) {
-          hipLaunchKernelGGL(k_scat_sweep, dim3(nc, sp), dim3(kBlock), lds_meta, cs, fa, part, sp,
+          hipLaunchKernelGGL(k_scat_sweep, dim3(nc, sp), dim3(kBlock), lds_scat, cs, fa, part, sp,
                              0);
           hipLaunchKernelGGL(k_scat_step, dim3(nc), dim3(64), 0, cs, fa, part, 0, ctrs, k & 1);
         }
@@ -781,7 +783,7 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
           for (int k = 0; k < kCheck; ++k) {
             const int init = it0 + k == 0 ? 1 : 0;
             if (int r = timed(ctx, PPF_K_SOLVE, [&] {
-                  hipLaunchKernelGGL(k_scat_sweep, dim3(nc, cur), dim3(kBlock), lds_meta,
+                  hipLaunchKernelGGL(k_scat_sweep, dim3(nc, cur), dim3(kBlock), lds_scat,
                                      ctx->stream, fa, part, cur, init);
                 }))
               return r;

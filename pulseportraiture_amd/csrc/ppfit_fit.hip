@@ -20,6 +20,7 @@
 namespace ppf {
 
 constexpr int NACC = 10;
+static_assert(NACC == kScatAcc, "k_scat_sweep's LDS rows (scat_sweep_lds)");
 constexpr double kTwoPi = 2.0 * kPi;
 constexpr double kFourPi2 = 4.0 * kPi * kPi;
 constexpr double kDconst2 = kDconst * kDconst;  // Dconst**2
@@ -143,12 +144,19 @@ __device__ __forceinline__ void block_sum_vec(double (&v)[N], double (*red)[48])
 constexpr int kPipe = 4;
 
 // cells in flight per lane in the scattering sweep and k_scat_sweep's
-// workgroups per CU (launch bound); A/B knobs for diagnostic builds
+// workgroups per CU (launch bound); A/B knobs for diagnostic builds.
+// r05: k_scat_sweep's two-phase evaluation (sweep_scat_split) needs 167
+// VGPRs at three workgroups per CU with no spills (the one-phase sweep: 223,
+// two): config 3 solve 13.26-13.28 -> 12.68-12.74 ms, fits bitwise the same
+// (U = 2 at three: 13.05-13.07; two-phase at two workgroups: 13.28)
 #ifndef PPF_SCAT_U
 #define PPF_SCAT_U 4
 #endif
+#ifndef PPF_SCAT_TWO_PHASE
+#define PPF_SCAT_TWO_PHASE 1
+#endif
 #ifndef PPF_SCAT_WG_PER_CU
-#define PPF_SCAT_WG_PER_CU 1
+#define PPF_SCAT_WG_PER_CU (PPF_SCAT_TWO_PHASE ? 3 : 1)
 #endif  // divides the 32-step re-seed period
 
 __device__ __forceinline__ void cells_phase(const double2* __restrict__ Xr, int J, int h,
@@ -1654,6 +1662,93 @@ __device__ __forceinline__ void scat_step_wave(const FitArgs& a, const double* p
   }
 }
 
+// k_scat_sweep's evaluation: sweep<0, true>'s arithmetic over channels
+// [j0, j1) in two phases.  Phase 1 runs every group's cell loop and parks the
+// group-summed accumulators in LDS (chA, one row per channel of the block);
+// phase 2, after a barrier, forms each channel's f / g / H terms from them.
+// The same numbers in the same order as the one-phase loop (the accumulators
+// pass through LDS unchanged), but nothing the terms need is live across the
+// cell loop: the loop's registers alone set the kernel's, not the loop's
+// plus everything derive() holds (223 VGPRs in one phase, two waves per SIMD).
+__device__ __forceinline__ void sweep_scat_split(const FitArgs& a, const Meta& m, int c, int s,
+                                                 const double* prm, const double* refs, double P,
+                                                 double* acc_slot, int j0, int j1, double* gpart,
+                                                 double* chA) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g8 = lane >> 3, h = lane & 7;
+  const int J = a.NHP >> 3;
+  const bool log10_tau = a.log10_tau != 0;
+  const int jend = min(m.nok, j1);
+  const int ngroups = (jend + 7) >> 3;
+  const int gfirst = (j0 >> 3) + w;
+  // phase 0: each channel's phase and tau_n (phase_frac, pow: the same calls
+  // on the same operands as in the loop, by one thread each) into chP, so
+  // the cell-loop phase carries neither
+  double2* chP = reinterpret_cast<double2*>(chA + (size_t)(((j1 - j0) + 7) & ~7) * NACC);
+  const bool scat = (log10_tau ? pow(10.0, prm[3]) : prm[3]) != 0.0;
+  for (int jl = tid; jl < jend - j0; jl += kBlock) {
+    const double fr = m.fr[j0 + jl];
+    const double tau_lin = log10_tau ? pow(10.0, prm[3]) : prm[3];
+    chP[jl] = cmk(phase_frac(prm, fr, refs, P), scat ? tau_lin * pow(fr / refs[2], prm[4]) : 0.0);
+  }
+  __syncthreads();
+  {
+    const int midx = a.model_idx ? a.model_idx[s] : 0;
+    for (int gi = gfirst; gi < ngroups; gi += kWaves) {
+      const int j = gi * 8 + g8;
+      const bool valid = j < jend;
+      const int jj = valid ? j : jend - 1;
+      const int n = m.chan[jj];
+      const double2 pt = chP[jj - j0];
+      const double2* Xr = a.X + ((size_t)c * a.nchan + n) * a.NHP;
+      double acc[NACC];
+      if (!scat) {
+        cells_phase(Xr, J, h, pt.x, acc);
+      } else {
+        const double* M2r = a.M2 + ((size_t)midx * a.nchan + n) * a.NHP;
+        cells_scat<PPF_SCAT_U>(Xr, M2r, J, h, pt.x, pt.y, acc);
+      }
+#pragma unroll
+      for (int i = 0; i < NACC; ++i) acc[i] = group8_sum(acc[i]);
+      if (h == 0 && valid) {
+        double* row = chA + (size_t)(j - j0) * NACC;
+        double* dst = acc_slot + (size_t)j * NACC;
+#pragma unroll
+        for (int i = 0; i < NACC; ++i) {
+          row[i] = acc[i];
+          dst[i] = acc[i];
+        }
+      }
+    }
+  }
+  __syncthreads();  // chA complete (and nothing below is hoisted above the cell loops)
+  const double tau_lin = log10_tau ? pow(10.0, prm[3]) : prm[3];
+  const int fm = flag_mask(a);
+  constexpr int NP = 21;
+  for (int gi = gfirst; gi < ngroups; gi += kWaves) {
+    const int j = gi * 8 + g8;
+    const bool valid = j < jend;
+    const int jj = valid ? j : jend - 1;
+    const double fr = m.fr[jj];
+    double acc[NACC];
+    const double* row = chA + (size_t)(jj - j0) * NACC;
+#pragma unroll
+    for (int i = 0; i < NACC; ++i) acc[i] = row[i];
+    const double dpre[2] = {m.d1[jj], m.d2[jj]};
+    const ChanDeriv d = derive<true>(acc, scat, m.pn[jj], m.iw2[jj], fr, prm, tau_lin, refs, P,
+                                     log10_tau, dpre);
+    const double q = d.C * d.C / d.S;
+    const LanePick L{d.dph[0], d.dph[1], d.dph[2], d.dts[0],
+                     d.dts[1], d.d2ts[0], d.d2ts[1], d.d2ts[2]};
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const double v = chan8_sum(valid ? mode0_term(d, L, q, h + 8 * r, fm) : 0.0);
+      const int t = (lane & 7) + 8 * r;
+      if (lane >= 8 && lane < 16 && t < NP) gpart[(size_t)gi * kScatPart + t] = v;
+    }
+  }
+}
+
 __global__ __launch_bounds__(kBlock, PPF_SCAT_WG_PER_CU) void k_scat_sweep(FitArgs a, double* part,
                                                                           int split, int init) {
   extern __shared__ __align__(16) unsigned char dyn[];
@@ -1672,9 +1767,17 @@ __global__ __launch_bounds__(kBlock, PPF_SCAT_WG_PER_CU) void k_scat_sweep(FitAr
   const double* prm = init ? st.x : st.xp;
   const int slot = init ? 0 : (st.slot ^ 1);
   double* acc = a.acc + ((size_t)c * 2 + slot) * a.nchan * NACC;
+#if PPF_SCAT_TWO_PHASE
+  // the block's channel rows of group sums (dynamic LDS after the Meta arrays)
+  double* chA = reinterpret_cast<double*>(dyn + scat_meta_lds(a.nchan));
+  if (j0 < j1)
+    sweep_scat_split(a, m, c, s, prm, st.refs, a.P[s], acc, j0, j1,
+                     part + (size_t)c * ((a.nchan + 7) >> 3) * kScatPart, chA);
+#else
   if (j0 < j1)
     sweep<0, true>(a, m, c, s, prm, st.refs, a.P[s], acc, sh.out, sh.red, TaylorSrc{}, nullptr,
                    j0, j1, part + (size_t)c * ((a.nchan + 7) >> 3) * kScatPart);
+#endif
   (void)tid;
 }
 

@@ -755,6 +755,18 @@ __global__ void k_scat_taus(const double* freqs, int n, double tau, double alpha
                             double* out);
 __global__ void k_guess(FitArgs a);
 constexpr int kScatPart = 24;  // split scattering sweep partial: f, g[5], H pairs[15], pad
+constexpr int kScatAcc = 10;   // cell-loop accumulators per channel (NACC)
+// k_scat_sweep's dynamic LDS: the Meta arrays, then (two-phase sweep) one row
+// of kScatAcc group sums per channel a block can take at the given split
+__host__ __device__ inline size_t scat_meta_lds(int nchan) {
+  return ((size_t)nchan * (5 * sizeof(double) + sizeof(int)) + 255) & ~(size_t)255;
+}
+__host__ __device__ inline size_t scat_sweep_lds(int nchan, int split) {
+  const int ng = (nchan + 7) >> 3;
+  // rows of kScatAcc sums, then one (phase, tau_n) pair per row
+  const size_t rows = (size_t)((ng + split - 1) / split) * 8;
+  return scat_meta_lds(nchan) + rows * (kScatAcc * sizeof(double) + 2 * sizeof(double));
+}
 __global__ void k_scat_sweep(FitArgs a, double* part, int split, int init);
 __global__ void k_scat_step(FitArgs a, const double* part, int init, int* ctrs, int par);
 __global__ void k_model_mean(const double2* M, double2* Mmean, int nchan, int NHP);
