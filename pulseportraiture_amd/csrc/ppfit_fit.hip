@@ -2411,7 +2411,14 @@ __device__ void post_subint(const FitArgs& a, int c, int s, unsigned char* dyn, 
 // A/B at config 2: four per CU (128 VGPRs, 77 spilled) 0.47 -> 0.56 ms (r02's
 // code had preferred the cap).  The scattering variant keeps its registers.
 template <bool SCAT>
-__global__ __launch_bounds__(kBlock, SCAT ? 1 : PPF_POST_WG_PER_CU) void k_post(FitArgs a) {
+#ifndef PPF_POST_SCAT_WG_PER_CU
+// two workgroups per CU (256 VGPRs, 12 B/lane spilled) instead of one (256 +
+// 7 AGPRs): config 3's k_post<true> 1.30 -> 1.09-1.10 ms, bitwise the same
+// (a two-phase with-scales sweep, 236 VGPRs unspilled, measured the same
+// and moved param_errs by an ulp: not kept)
+#define PPF_POST_SCAT_WG_PER_CU 2
+#endif
+__global__ __launch_bounds__(kBlock, SCAT ? PPF_POST_SCAT_WG_PER_CU : PPF_POST_WG_PER_CU) void k_post(FitArgs a) {
   extern __shared__ __align__(16) unsigned char dyn[];
   __shared__ PostShared sh;
   const int c = blockIdx.x, s = a.sub0 + c;
