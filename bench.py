@@ -73,7 +73,7 @@ KERNEL_SYMBOL = {"solve": "k_scat_sweep", "data_xspec": "k_data_xspec<10>",
 # ppalign with the data-spectrum cache (ppalign.SPEC_CACHE): the rotate-and-sum
 # and the fit read the cached spectra
 KERNEL_SYMBOL_PPALIGN = dict(KERNEL_SYMBOL, rot_accum="k_rot_accum_spec",
-                             fit_taylor="k_fit_taylor<false, true>", guess="k_guess")
+                             fit_taylor="k_fit_taylor<true, true>", guess="k_guess")
 # align_archives calls in one `bench.py --config ppalign` run (warm-up, two
 # timed, one with kernel timing): PMC bytes per call = all launches / this
 PPALIGN_CALLS = 4
