@@ -663,8 +663,16 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
               launch_fit_taylor(ctx, dim3(n), lds_taylor, st, fp);
             }))
           return r;
+        // subints the Taylor path does not take (tau != 0 at the start, not
+        // fitted): the one-workgroup scattering solve and post-fit, as on
+        // one queue (both exit at once for every other subint)
+        if (int r = timed_on(ctx, PPF_K_SOLVE, st, [&] {
+              hipLaunchKernelGGL(k_solve<true>, dim3(n), dim3(kBlock), lds_meta, st, fp);
+            }))
+          return r;
         if (int r = timed_on(ctx, PPF_K_POST, st, [&] {
               hipLaunchKernelGGL(k_post<false>, dim3(n), dim3(kBlock), lds_meta, st, fp);
+              hipLaunchKernelGGL(k_post<true>, dim3(n), dim3(kBlock), lds_meta, st, fp);
             }))
           return r;
         if (o->errs_out)

@@ -95,10 +95,15 @@ def test_recentring_bitwise(gpu):
 
 
 def test_pieces_schedule_bitwise(gpu):
-    c = _case(gpu, 48, 64, 2048, 9191)
+    """The two-queue piece schedule (ppf_set_pipeline), with and without the
+    cache, and with subints the Taylor path does not take among the pieces
+    (their scattering solve and post-fit run per piece as on one queue)."""
+    c = _case(gpu, 48, 64, 2048, 9191, scat_rows=(3, 30))
     base = _fit(gpu, c, c["models"][0])
+    assert (base["status"][[3, 30]] >= 0).all() and (base["nfev"][[3, 30]] > 0).all()
     gpu.set_pipeline(3)
     try:
+        _same(base, _fit(gpu, c, c["models"][0]))
         sc = gpu.spec_cache(*c["data"].shape)
         _same(base, _fit(gpu, c, c["models"][0], spec=sc))
         _same(base, _fit(gpu, c, c["models"][0], spec=sc))
