@@ -1799,64 +1799,103 @@ __global__ __launch_bounds__(64) void k_scat_step(FitArgs a, const double* part,
 // The post-fit's serial sections (thread 0) index small arrays at run time;
 // they live in the block's LDS workspace (PostWs), not in per-lane scratch.
 struct PostWs {
-  double c[7], pol[7][7], prev[7], pts[9], cur[7];  // poly_real_roots
-  double roots[7], co[7];                          // closest_positive / nz_solve
+  double c[7], pol[7][7], prev[7], pts[9], cur[7], brk[8];  // poly_real_roots
+  double bound;
+  int kind[8], d, np, npts, deg;
+  double co[7], nz[3];                                      // nz_solve
   double M[5][10];                                 // invert_small
   double A[25], Ci[25];                            // with-scales / no-scales blocks
 };
 
 // Real roots of sum_i c[i] y^(deg-i) (deg <= 6) in ascending order: the roots
 // of the derivative bracket them; each bracket is bisected to convergence.
-__device__ int poly_real_roots(const double* cin, int deg, double* roots, PostWs& w) {
-  double* c = w.c;
-  int off = 0;
-  while (off <= deg && cin[off] == 0.0) ++off;  // np.roots strips leading zeros
-  int d = deg - off;
-  for (int i = 0; i <= d; ++i) c[i] = cin[off + i];
-  while (d > 0 && c[d] == 0.0) --d;             // trailing zeros: roots at 0 (not > 0)
-  if (d <= 0) return 0;
+// All threads of the block call it (uniform deg): thread 0 builds the
+// derivative ladder and the brackets of each level, thread q bisects bracket
+// q, and thread 0 gathers the level's roots in bracket order -- the same
+// arithmetic, per bracket, as a serial sweep, so the roots are bitwise those
+// of one.  Returns the root count (block-uniform); roots in w.prev.
+__device__ int poly_real_roots(const double* cin, int deg, PostWs& w, int tid) {
   auto& pol = w.pol;
-  for (int i = 0; i <= d; ++i) pol[d][i] = c[i] / c[0];
-  for (int o = d - 1; o >= 1; --o)
-    for (int i = 0; i <= o; ++i) pol[o][i] = pol[o + 1][i] * (double)(o + 1 - i) / (double)(o + 1);
-  double bound = 0.0;
-  for (int i = 1; i <= d; ++i) bound = fmax(bound, fabs(pol[d][i]));
-  bound = 1.0 + bound;
-  double* prev = w.prev;
-  int np_ = 1;
-  prev[0] = -pol[1][1];  // linear
+  if (tid == 0) {
+    double* c = w.c;
+    int off = 0;
+    while (off <= deg && cin[off] == 0.0) ++off;  // np.roots strips leading zeros
+    int d = deg - off;
+    for (int i = 0; i <= d; ++i) c[i] = cin[off + i];
+    while (d > 0 && c[d] == 0.0) --d;             // trailing zeros: roots at 0 (not > 0)
+    w.d = d;
+    if (d > 0) {
+      for (int i = 0; i <= d; ++i) pol[d][i] = c[i] / c[0];
+      for (int o = d - 1; o >= 1; --o)
+        for (int i = 0; i <= o; ++i)
+          pol[o][i] = pol[o + 1][i] * (double)(o + 1 - i) / (double)(o + 1);
+      double bound = 0.0;
+      for (int i = 1; i <= d; ++i) bound = fmax(bound, fabs(pol[d][i]));
+      w.bound = 1.0 + bound;
+      w.prev[0] = -pol[1][1];  // linear
+      w.np = 1;
+    } else {
+      w.np = 0;
+    }
+  }
+  __syncthreads();
+  const int d = w.d;
   for (int o = 2; o <= d; ++o) {
-    double* pts = w.pts;
-    int npts = 0;
-    pts[npts++] = -bound;
-    for (int i = 0; i < np_; ++i) pts[npts++] = fmin(fmax(prev[i], -bound), bound);
-    pts[npts++] = bound;
-    double* cur = w.cur;
-    int nc = 0;
     auto ev = [&](double x) {
       double v = pol[o][0];
       for (int i = 1; i <= o; ++i) v = v * x + pol[o][i];
       return v;
     };
-    for (int q = 0; q + 1 < npts; ++q) {
-      double lo = pts[q], hi = pts[q + 1];
-      double flo = ev(lo), fhi = ev(hi);
-      if (flo == 0.0) { if (nc == 0 || cur[nc - 1] != lo) cur[nc++] = lo; continue; }
-      if ((flo < 0.0) == (fhi < 0.0)) continue;
-      for (int it = 0; it < 200; ++it) {
-        const double mid = 0.5 * (lo + hi);
-        if (mid == lo || mid == hi) break;
-        const double fm = ev(mid);
-        if ((fm < 0.0) == (flo < 0.0)) { lo = mid; flo = fm; } else { hi = mid; }
-      }
-      cur[nc++] = 0.5 * (lo + hi);
+    if (tid == 0) {
+      const double bound = w.bound;
+      double* pts = w.pts;
+      int npts = 0;
+      pts[npts++] = -bound;
+      for (int i = 0; i < w.np; ++i) pts[npts++] = fmin(fmax(w.prev[i], -bound), bound);
+      pts[npts++] = bound;
+      w.npts = npts;
     }
-    if (ev(bound) == 0.0) cur[nc++] = bound;
-    np_ = nc;
-    for (int i = 0; i < nc; ++i) prev[i] = cur[i];
+    __syncthreads();
+    if (tid + 1 < w.npts) {
+      double lo = w.pts[tid], hi = w.pts[tid + 1];
+      double flo = ev(lo);
+      const double fhi = ev(hi);
+      int kind = 0;  // 0: no root, 1: root at lo, 2: bisected root
+      double r = lo;
+      if (flo == 0.0) {
+        kind = 1;
+      } else if ((flo < 0.0) != (fhi < 0.0)) {
+        for (int it = 0; it < 200; ++it) {
+          const double mid = 0.5 * (lo + hi);
+          if (mid == lo || mid == hi) break;
+          const double fm = ev(mid);
+          if ((fm < 0.0) == (flo < 0.0)) { lo = mid; flo = fm; } else { hi = mid; }
+        }
+        kind = 2;
+        r = 0.5 * (lo + hi);
+      }
+      w.kind[tid] = kind;
+      w.brk[tid] = r;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double* cur = w.cur;
+      int nc = 0;
+      for (int q = 0; q + 1 < w.npts; ++q) {
+        const int kind = w.kind[q];
+        if (kind == 1) {
+          if (nc == 0 || cur[nc - 1] != w.brk[q]) cur[nc++] = w.brk[q];
+        } else if (kind == 2) {
+          cur[nc++] = w.brk[q];
+        }
+      }
+      if (ev(w.bound) == 0.0) cur[nc++] = w.bound;
+      w.np = nc;
+      for (int i = 0; i < nc; ++i) w.prev[i] = cur[i];
+    }
+    __syncthreads();
   }
-  for (int i = 0; i < np_; ++i) roots[i] = prev[i];
-  return np_;
+  return w.np;
 }
 
 // Gauss-Jordan inverse with partial pivoting (np.linalg.inv), n <= 5.
@@ -2047,10 +2086,8 @@ __device__ __forceinline__ void block_sum_first(double (&v)[22], double (*red)[4
   for (int i = 0; i < N; ++i) v[i] = u[i];
 }
 
-__device__ double closest_positive(const double* coeffs, int deg, bool sq, double fmean,
-                                   PostWs& w) {
-  double* r = w.roots;
-  const int nr = poly_real_roots(coeffs, deg, r, w);
+// the positive root (sqrt of it when sq) closest to fmean
+__device__ double closest_positive(const double* r, int nr, bool sq, double fmean) {
   double best = NAN, bd = INFINITY;
   for (int i = 0; i < nr; ++i) {
     if (!(r[i] > 0.0)) continue;
@@ -2062,8 +2099,9 @@ __device__ double closest_positive(const double* coeffs, int deg, bool sq, doubl
 }
 
 // Solve the branch from the channel sums t[22]; writes nz[3] (refs preset).
-__device__ void nz_solve(int br, int option, const double* t, double fmean, double* nz,
-                         PostWs& w) {
+// The GM branches leave a polynomial in y = nu^2 in w.co and return its
+// degree: the block's root finder and closest_positive finish them.
+__device__ int nz_solve(int br, int option, const double* t, double* nz, PostWs& w) {
   switch (br) {
     case NZ_PD: nz[0] = pow(t[0] / t[1], -0.5); break;
     case NZ_PG: nz[1] = pow(t[0] / t[1], -0.25); break;
@@ -2084,8 +2122,7 @@ __device__ void nz_solve(int br, int option, const double* t, double fmean, doub
         cy[1] = E * Hh - A * D;
         cy[2] = F * G - B * C;
         cy[3] = B * D - F * Hh;
-        const double x = closest_positive(cy, 3, true, fmean, w);
-        nz[0] = nz[1] = x;
+        return 3;
       }
     } break;
     case NZ_PDTA: {
@@ -2126,12 +2163,12 @@ __device__ void nz_solve(int br, int option, const double* t, double fmean, doub
           co[4] = -a * a * b + a * c * f;
           deg = 4;
         }
-        const double x = closest_positive(co, deg, true, fmean, w);
-        nz[0] = nz[1] = x;
+        return deg;
       }
     } break;
     default: break;
   }
+  return 0;
 }
 
 struct PostShared {
@@ -2241,11 +2278,19 @@ __device__ void post_subint(const FitArgs& a, int c, int s, unsigned char* dyn, 
       case 22: block_sum_first<22>(sums, sh.red); break;
       default: break;
     }
+    double* nz = sh.ws.nz;  // thread 0's, in LDS: no registers live across the root finder
     if (tid == 0) {
-      double nz[3] = {sh.refs[0], sh.refs[1], sh.refs[2]};
-      nz_solve(br, a.option, sums, sh.fmean, nz, sh.ws);
-      for (int i = 0; i < 3; ++i) if (isnan(nuo[i])) nuo[i] = nz[i];
+      for (int i = 0; i < 3; ++i) nz[i] = sh.refs[i];
+      sh.ws.deg = nz_solve(br, a.option, sums, nz, sh.ws);
     }
+    __syncthreads();
+    const int pdeg = sh.ws.deg;
+    if (pdeg > 0) {
+      const int nr = poly_real_roots(sh.ws.co, pdeg, sh.ws, tid);
+      if (tid == 0) nz[0] = nz[1] = closest_positive(sh.ws.prev, nr, true, sh.fmean);
+    }
+    if (tid == 0)
+      for (int i = 0; i < 3; ++i) if (isnan(nuo[i])) nuo[i] = nz[i];
   }
   mark(17);
   if (tid == 0) {
