@@ -208,3 +208,43 @@ def test_open_archive_reads_ranges(gpu):
         np.testing.assert_allclose(part, whole[2:5], rtol=0, atol=1e-13 * np.abs(whole).max())
     # the registered device tensor itself is never modified
     assert np.array_equal(archive._registry["rng_dev"].subints.cpu().numpy(), b["subints"])
+
+
+@pytest.mark.parametrize("sparse", [False, True])
+def test_get_toas_pieces_equal_one_piece(gpu, tmp_path, sparse):
+    """Device-resident subints fitted in pipeline pieces (pipeline_fracs: the
+    pieces' columns concatenated by _finish) give the per-archive columns and
+    .tim text of one piece; sparse: one subint with no weight, so ok_isubs
+    skips it (the spread into nsub rows)."""
+    import torch
+    from pulseportraiture_amd import archive, pplib, pptoas, synth
+    w, b = _bunch(nsub=40, nchan=16, nbin=256, seed=21)
+    if sparse:
+        b["weights"][7] = 0.0
+    b["subints"] = torch.as_tensor(b["subints"], device="cuda")
+    archive.register_archive("pieces", b)
+    shutil.copy(synth.EXAMPLE_GMODEL, str(tmp_path / "example.gmodel"))
+    cwd = os.getcwd()
+    os.chdir(tmp_path)
+    try:
+        out, tims = [], []
+        for mins in (1 << 30, 8):
+            gt = pptoas.GetTOAs(["pieces"], "example.gmodel", quiet=True)
+            gt.pipeline_min_subints = mins
+            gt.get_TOAs(quiet=True)
+            tim = str(tmp_path / ("p%d.tim" % mins))
+            pplib.write_TOAs(gt.TOA_list, SNR_cutoff=0.0, outfile=tim, append=False)
+            out.append(gt)
+            tims.append(open(tim).read())
+    finally:
+        os.chdir(cwd)
+        archive.unregister_archive("pieces")
+    one, two = out
+    assert len(two.shard_blocks) == 2  # really two pieces
+    assert len(one.ok_isubs[0]) == (39 if sparse else 40)
+    for attr in ("phis", "phi_errs", "DMs", "DM_errs", "scales", "scale_errs", "channel_snrs",
+                 "snrs", "red_chi2s", "covariances", "nfevals", "rcs", "nu_refs", "TOA_errs"):
+        a, c = np.asarray(getattr(one, attr)[0]), np.asarray(getattr(two, attr)[0])
+        assert a.shape == c.shape, attr
+        assert np.array_equal(a.astype(np.float64), c.astype(np.float64), equal_nan=True), attr
+    assert tims[0] == tims[1]
