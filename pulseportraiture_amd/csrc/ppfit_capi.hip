@@ -103,7 +103,8 @@ int check_nbin(ppf_ctx* ctx, int nbin, int* logN) {
   return PPF_OK;
 }
 
-int nharm_pad(int nbin) { return ((nbin / 2 + 1) + 7) & ~7; }
+// rows of 16 cells (256 B): measured faster than 8 or 32
+int nharm_pad(int nbin) { return ((nbin / 2 + 1) + 15) & ~15; }
 
 // get_noise_PS: kc = int((1 - 1/4) * nharm) (pplib.py:2245)
 int noise_kc(int nbin) { return (int)(0.75 * (double)(nbin / 2 + 1)); }
