@@ -82,11 +82,6 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 // phi_c} per step pair.  A multiple of every tile's U, so the 16- and
 // 8-channel tiles re-seed at the same harmonics (bitwise the same moments).
 constexpr int kMomReseedSteps = 8;
-#ifndef PPF_VPOW_DIAG
-// 1: a diagnostic build (wrong moments) whose power-table reads stay within
-// 16 rows, to attribute the moment pass's L2-miss traffic by PMC
-#define PPF_VPOW_DIAG 0
-#endif
 
 // X rows: plain loads (the non-temporal hint measured slower here)
 __device__ __forceinline__ double2 xload(const double2* p) { return *p; }
@@ -199,11 +194,7 @@ __device__ __forceinline__ void moment_tile16(const FitArgs& a, int c, int slot,
         const int t = 2 * u + h;
         xb[t] = xload(Xr + min(4 * ((b + 1) * U + t) + kk, N));
         if constexpr (DSP) mb[t] = Mr[min(4 * ((b + 1) * U + t) + kk, N)];
-#if PPF_VPOW_DIAG  // diagnostic build only (PMC): the power rows of 16 steps, reused
-        pb[t] = vp[(size_t)(((b + 1) * U + t) & 15) * 64];
-#else
         pb[t] = vp[(size_t)((b + 1) * U + t) * 64];
-#endif
       }
     }
   }

@@ -969,6 +969,13 @@ class SpecCache:
     def nbytes(self):
         return sum(t.numel() * 8 for t in (self.spec, self.sig, self.dsum, self.R))
 
+    @staticmethod
+    def bytes_for(eng, nsub, nchan, nbin):
+        """What __init__ allocates for this shape (NHP from the library, so
+        the estimate follows its row padding)."""
+        nhp = int(eng.lib.ppf_spec_nhp(int(nbin)))
+        return (nsub * nchan * nhp + nsub * nhp) * 16 + 2 * nsub * nchan * 8
+
 
 def get_engine(device=None):
     """Process-wide engine per device."""

@@ -596,7 +596,8 @@ class _UnitStack:
         d = self.pols[0]
         if SPEC_CACHE and isinstance(d, torch.Tensor) and d.device.type == "cuda":
             n, nchan, nbin = d.shape
-            need = (n * nchan * (nbin // 2 + 9) + n * (nbin // 2 + 9)) * 16 + 2 * n * nchan * 8
+            from .engine import SpecCache
+            need = SpecCache.bytes_for(eng, n, nchan, nbin)
             free, _ = torch.cuda.mem_get_info(d.device)
             if need < 0.75 * free:
                 sc = eng.spec_cache(n, nchan, nbin)

@@ -39,7 +39,9 @@ def _dist_info():
 def _gc_paused(fn):
     """Run fn with Python's cyclic collector paused: get_TOAs makes few
     containers, but a full collection of the caller's heap (a torch process
-    holds ~10^5 objects) landing inside the call costs more than the call."""
+    holds ~10^5 objects) landing inside the call costs more than the call.
+    The young generations are still collected after every fitted piece
+    (_collect), so garbage does not accumulate over a long call."""
     import functools
 
     @functools.wraps(fn)
@@ -384,16 +386,17 @@ class GetTOAs:
                 if rank != 0:  # the results live on rank 0
                     del self.ok_idatafiles[n_ok0:]
                     return
-            shards, durations = {}, {}
+            shards, spans = {}, {}
             for s_r, d_r in got:
                 for ij, v in s_r.items():
                     shards.setdefault(ij, []).extend(v)
-                for ij, t in d_r.items():
-                    durations[ij] = durations.get(ij, 0.0) + t
+                for ij, sp in d_r.items():  # summed over the ranks fitting the archive
+                    spans[ij] = spans.get(ij, 0.0) + sp[1] - sp[0]
+        else:
+            spans = {ij: sp[1] - sp[0] for ij, sp in durations.items()}
         t = mark("gather", t)
         for ij, job in enumerate(jobs):
-            self._finish(job, sorted(shards[ij], key=lambda v: v.a0),
-                         durations.get(ij, 0.0), quiet)
+            self._finish(job, sorted(shards[ij], key=lambda v: v.a0), spans.get(ij, 0.0), quiet)
         mark("finish", t)
         tot = time.time() - start
         if not quiet and len(self.ok_isubs):
@@ -1009,12 +1012,21 @@ class GetTOAs:
             return
         del pend[key]
         ij, a0 = key
-        durations[ij] = durations.get(ij, 0.0) + time.time() - p[3]
+        # the archive's fit wall time on this rank: first submit to last
+        # collect (its pieces overlap on the device, so no per-piece sum)
+        t0, t1 = durations.get(ij, (p[3], p[3]))
+        durations[ij] = (min(t0, p[3]), max(t1, time.time()))
         sh = self._shard(jobs[ij], a0, out, *toa_args)
         t = mark("shard", t)
         sh.block.preformat()  # the .tim text of these records
         mark("preformat", t)
         shards.setdefault(ij, []).append(sh)
+        # the collector is paused over get_TOAs (_gc_paused): free this
+        # piece's cyclic garbage from the young generations, so a long call
+        # (a 125k-subint shard in many pieces) does not pile it up, without
+        # a full collection of the caller's heap inside the call
+        if not gc.isenabled():
+            gc.collect(1)
 
     def _shard(self, job, a0, res, print_phase, print_flux, print_parangle, addtnl_toa_flags):
         """Columns of ok subints job.ok_isubs[a0:a0 + n] from their device
@@ -1259,10 +1271,11 @@ class _Job(DataBunch):
     def row(self, key, s):
         """Per-subint [nsub, nchan] input key ("freqs", "weights", "mask")
         for subints s: one shared [nchan] row when every subint's is the
-        same."""
+        same.  The shared row is the first ok subint's: `uniform` compares
+        the ok subints' rows only, and a zapped subint 0 is not one of them."""
         a = self.mask if key == "mask" else self.data[key]
         if self.uniform[key]:
-            return a[0]
+            return a[int(self.ok_isubs[0])]
         return _take(a, s)
 
 

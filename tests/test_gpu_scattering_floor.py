@@ -26,11 +26,13 @@ Asserted, per subint:
 * |chi^2_device - chi^2_reference| <= 1e-3;
 * the end point is within 1e-3 sigma of the reference's, or of one of the
   reference's own end points under a one-ulp restart or a channel
-  reordering, or -- where the device stops between them -- no farther from
-  the reference than the reference's own spread;
+  reordering -- no "between them" category: a device end point the
+  reference never reaches fails;
 * where the reference's own spread is below 1e-3 sigma, within 1e-3 sigma of
   the reference.
 And over the set, a bar that does not move with the device's results:
+* at most ON_ALT_MAX (24, the count at r05) subints are on an alternate end
+  point of the reference's only;
 * the alternate set is frozen at the 4 restarts + 24 reorderings committed
   in r04 (asserted: 24 orderings);
 * the device agrees with the reference (within 1e-3 sigma) on at least as
@@ -51,6 +53,7 @@ from tests.golden_consts import DM0
 pytestmark = pytest.mark.gpu
 
 PARAMS = ["phi", "DM", "tau", "alpha"]
+ON_ALT_MAX = 24  # subints on a reference end point other than its own (r05: 24 of 200)
 
 
 @pytest.fixture(scope="module")
@@ -97,7 +100,6 @@ def test_scattering_200_subints_vs_reference(gpu):
     dchi2 = (r["red_chi2"] - z["red_chi2"]) * dof
     near = dx <= 1e-3
     on_alt = to_alt <= 1e-3
-    within = dx <= 1e-3 + 1.05 * spread
     dn = r["nfev"] - z["nfev"].astype(int)
     print("config 3, %d subints: %d within 1e-3 sigma of the reference (max %.3g), %d more on "
           "one of the reference's own end points, %d between them; reference's own spread > "
@@ -111,7 +113,8 @@ def test_scattering_200_subints_vs_reference(gpu):
                   i, dx[i], to_alt[i], spread[i], r["nfev"][i], z["nfev"][i], dchi2[i]))
     assert np.abs(dchi2).max() <= 1e-3
     assert np.abs(dn).max() <= 2, np.where(np.abs(dn) > 2)
-    assert (near | on_alt | within).all(), np.where(~(near | on_alt | within))
+    assert (near | on_alt).all(), np.where(~(near | on_alt))
+    assert (on_alt & ~near).sum() <= ON_ALT_MAX, np.where(on_alt & ~near)
     stable = spread <= 1e-3
     assert near[stable].all(), np.where(stable & ~near)
     # the statistical bar: the reference's own agreement rate per ordering

@@ -150,6 +150,43 @@ def test_bulk_text_equals_per_toa_text(kw):
     assert bulk == _per_toa(gt)
 
 
+def test_zapped_first_subint_shared_rows():
+    """Subint 0 fully zapped and every other subint sharing one weights row:
+    the one row handed to the fits is an ok subint's, not subint
+    0's all-zero row (nor its frequencies) -- every fitted channel keeps its
+    scale, and the ok subints' results equal those of the same archive
+    without subint 0."""
+    from pulseportraiture_amd import archive, synth
+    from pulseportraiture_amd.mjd import MJD
+    nsub, nchan = 5, 8
+    w = synth.make_workload(nsub, nchan, 64, seed=91)
+    data = synth.workload_data_host(w)
+    out = []
+    for name, s0 in (("zap0.npz", 0), ("zap0_dropped.npz", 1)):
+        wts = np.ones((nsub, nchan))
+        wts[:, 5] = 0.25
+        wts[0] = 0.0
+        freqs = np.tile(w.freqs, (nsub, 1))
+        freqs[0] += 1.0  # subint 0's own row differs too
+        archive.register_archive(name, dict(
+            subints=data[s0:, None], freqs=freqs[s0:], Ps=np.full(nsub - s0, w.P),
+            weights=wts[s0:], noise_stds=np.full((nsub - s0, 1, nchan), 1.5),
+            epochs=[MJD(57000.0 + 0.37 * k) for k in range(s0, nsub)], DM=DM0, backend="be",
+            frontend="fe", telescope="GBT", telescope_code="1",
+            parallactic_angles=np.zeros(nsub - s0), subtimes=[60.0] * (nsub - s0)))
+        try:
+            out.append(_get_toas([name]))
+        finally:
+            archive.unregister_archive(name)
+    a, b = out
+    assert list(a.ok_isubs[0]) == [1, 2, 3, 4] and list(b.ok_isubs[0]) == [0, 1, 2, 3]
+    sc = np.asarray(a.scales[0])
+    assert (sc[1:] > 0).all() and not sc[0].any()
+    for attr in ("phis", "DMs", "scales", "channel_snrs", "nu_refs", "snrs"):
+        assert np.array_equal(np.asarray(getattr(a, attr)[0], float)[1:],
+                              np.asarray(getattr(b, attr)[0], float), equal_nan=True), attr
+
+
 def test_flag_maps_and_types():
     """TOA objects built from the columns carry the reference's flag order and
     Python types (ints %d, floats, strings; None kept in the dict)."""
