@@ -50,6 +50,11 @@ CONFIGS = {
     "gm_shard": (125000, 128, 2048, [1, 1, 1, 0, 0], 0.0, False, 0.0,
                  "config 4 per-GPU shard: 125000 subints x 128 chan x 2048 bin, phase+DM+GM, "
                  "generated on the device chunk by chunk inside the timed region"),
+    "gm_shard_host": (125000, 128, 2048, [1, 1, 1, 0, 0], 0.0, False, 0.0,
+                      "config 4 per-GPU shard from host memory: 125000 subints x 128 chan x "
+                      "2048 bin, phase+DM+GM; int16 samples (PSRFITS DATA) + DAT_SCL / "
+                      "DAT_OFFS in pinned host memory, copied over PCIe, unpacked on the "
+                      "device (ppf_unpack_subints) and fitted, chunk by chunk"),
     "get_toas": (10000, 64, 2048, [1, 1, 0, 0, 0], 0.0, False, 0.0,
                  "GetTOAs.get_TOAs end to end: registered 10000 x 64 x 2048 archive, "
                  "TOA records + .tim text"),
@@ -57,6 +62,7 @@ CONFIGS = {
                 "config 5: align_archives, 4096 archives x 256 chan x 2048 bin, niter 3"),
 }
 TIMING_KEY = {"headline": "headline", "get_toas": "headline", "gm": "gm", "gm_shard": "gm",
+              "gm_shard_host": "gm",
               "scattering": "scattering", "ppalign": "ppalign"}
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
@@ -121,8 +127,10 @@ def parse():
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP events")
     ap.add_argument("--no-legs", action="store_true",
                     help="headline only: skip the get_toas / ppalign legs")
-    ap.add_argument("--shard-chunk", type=int, default=25000,
-                    help="gm_shard: subints generated and fitted per chunk")
+    ap.add_argument("--shard-chunk", type=int, default=None,
+                    help="gm_shard: subints generated and fitted per chunk (default 25000); "
+                         "gm_shard_host: subints copied, unpacked and fitted per chunk "
+                         "(default 16384: 8 GiB of int16 samples)")
     ap.add_argument("--ppalign-narch", type=int, default=4096)
     ap.add_argument("--ppalign-niter", type=int, default=3)
     ap.add_argument("--no-spec-cache", action="store_true",
@@ -433,7 +441,7 @@ def main():
     fit_config = "headline" if config == "get_toas" else config
     if args.cpu_sample is None:
         args.cpu_sample = {"headline": 150, "gm": 60, "scattering": 4, "get_toas": 0,
-                           "ppalign": 0, "gm_shard": 16}[config]
+                           "ppalign": 0, "gm_shard": 16, "gm_shard_host": 16}[config]
     eng = Engine(local if world > 1 else 0)
     E._engines[eng.device.index] = eng  # the drivers' get_engine() uses this context
     for o in args.opt:
@@ -444,6 +452,8 @@ def main():
         return main_ppalign(args, eng, rank, world)
     if config == "gm_shard":
         return main_gm_shard(args, eng, rank, world)
+    if config == "gm_shard_host":
+        return main_gm_shard_host(args, eng, rank, world)
 
     # ---- synthetic inputs, resident in HBM before timing ----
     w, data, kw, tau_g = synth_inputs(eng, fit_config, nsub, args.seed, rank * nsub)
@@ -530,7 +540,10 @@ def main():
         legs["get_toas"] = g
         legs["get_toas_host"], _ = leg_get_toas(eng, w, data, reps=1, host=True)
         legs["ppalign"] = leg_ppalign(eng, args.ppalign_narch, args.ppalign_niter, args.seed)
-        legs["ppalign"].pop("_ktimes", None)
+        from pulseportraiture_amd import ppalign as _ppa
+        legs["ppalign"]["roofline"] = ppalign_roofline(
+            legs["ppalign"].pop("_ktimes"), args.ppalign_narch, args.ppalign_niter,
+            _ppa.SPEC_CACHE)
 
     if rank != 0:
         if world > 1:
@@ -701,7 +714,7 @@ def main_gm_shard(args, eng, rank, world):
     from pulseportraiture_amd import synth, pplib
     nsub0, nchan, nbin, flags, _, _, _, desc = CONFIGS["gm_shard"]
     N = args.nsub or nsub0
-    C = min(args.shard_chunk, N)
+    C = min(args.shard_chunk or 25000, N)
     base = rank * N
     dev = eng.device
     w0 = synth.make_workload(1, nchan, nbin, seed=args.seed)
@@ -859,6 +872,199 @@ def main_gm_shard(args, eng, rank, world):
         torch.distributed.destroy_process_group()
 
 
+def main_gm_shard_host(args, eng, rank, world):
+    """--config gm_shard_host: config 4's per-GPU shard (125,000 x 128 x
+    2048) as a PSRFITS reader hands it over: the samples as int16 (PSRFITS
+    DATA) with per-(subint, channel) DAT_SCL / DAT_OFFS, resident in pinned
+    host memory (pptoas.py:246,343 reads every archive of the shard; the
+    native reader returns DATA undecoded, psrfits.py).  Inside the timed
+    region, chunk by chunk: the int16 samples and scales cross PCIe on a copy
+    queue (two device buffers: chunk i + 1 copies while chunk i is unpacked
+    and fitted), ppf_unpack_subints forms DATA * DAT_SCL + DAT_OFFS on the
+    device, fit_batch fits phase+DM+GM with get_TOAs' guess, the per-TOA
+    results go to pinned host memory.  Before timing the "archive" is made
+    on the device (k_synth, as --config gm_shard) and quantised to int16.
+    Reported beside the rate: the PCIe GB/s of the copies, each side's own
+    event time, and a parity sample (the oracle refits the dequantised
+    samples the device fitted)."""
+    import torch
+    from pulseportraiture_amd import synth, pplib
+    nsub0, nchan, nbin, flags, _, _, _, desc = CONFIGS["gm_shard_host"]
+    N = args.nsub or nsub0
+    C = min(args.shard_chunk or 16384, N)
+    base = rank * N
+    dev = eng.device
+    w0 = synth.make_workload(1, nchan, nbin, seed=args.seed)
+    nu_fit = pplib.guess_fit_freq(w0.freqs)
+    model = torch.as_tensor(w0.model, device=dev)
+    freqs = torch.as_tensor(w0.freqs, device=dev)
+    starts = list(range(0, N, C))
+    f64 = dict(dtype=torch.float64, device=dev)
+    # 1. the archive in host memory (before timing): each chunk generated on
+    # the device, quantised to int16 with DAT_SCL / DAT_OFFS per profile as
+    # PSRFITS stores it, copied to pinned host memory
+    gbuf = torch.empty((C, nchan, nbin), **f64)
+    hraw, t_prep = [], time.perf_counter()
+    hscl = torch.empty((N, 1, nchan), dtype=torch.float64, pin_memory=True)
+    hoff = torch.empty((N, 1, nchan), dtype=torch.float64, pin_memory=True)
+    for ci, s0 in enumerate(starts):
+        n = min(C, N - s0)
+        ph = torch.as_tensor(synth.make_workload(n, nchan, nbin, seed=args.seed,
+                                                 sub0=base + s0).phase, device=dev)
+        x = gbuf[:n]
+        eng.synth(w0.template, ph, w0.sigma, args.seed, sub0=base + s0, out=x)
+        mn, mx = x.amin(-1), x.amax(-1)
+        scl = (mx - mn) / 65534.0
+        scl = torch.where(scl > 0, scl, torch.ones_like(scl))
+        off = 0.5 * (mx + mn)
+        q = x.sub_(off[..., None]).div_(scl[..., None]).round_().clamp_(-32767, 32767) \
+            .to(torch.int16)
+        h = torch.empty((n, 1, nchan, nbin), dtype=torch.int16, pin_memory=True)
+        h.view(n, nchan, nbin).copy_(q)
+        hscl[s0:s0 + n, 0].copy_(scl)
+        hoff[s0:s0 + n, 0].copy_(off)
+        hraw.append(h)
+        del q
+        print("gm_shard_host: archive chunk %d/%d in host memory (%.0f s)" % (
+            ci + 1, len(starts), time.perf_counter() - t_prep), file=sys.stderr, flush=True)
+    del gbuf
+    torch.cuda.synchronize()
+    # 2. device buffers: two int16 chunks (+ scales), one unpacked chunk
+    nb = 2 if len(starts) > 1 else 1
+    draw = [torch.empty((C, 1, nchan, nbin), dtype=torch.int16, device=dev) for _ in range(nb)]
+    dscl = [torch.empty((C, 1, nchan), **f64) for _ in range(nb)]
+    doff = [torch.empty((C, 1, nchan), **f64) for _ in range(nb)]
+    fbuf = torch.empty((C, 1, nchan, nbin), **f64)
+    P = torch.full((C,), w0.P, **f64)
+    init = torch.tensor([[0.0, w0.DM0, 0.0, 0.0, 0.0]] * C, **f64)
+    nu = torch.full((C, 3), nu_fit, **f64)
+    small = ["params", "param_errs", "status", "nfev"]
+    host = {k: torch.empty((N,) + ((5,) if k.startswith("param") else ()),
+                           dtype=torch.float64 if k.startswith("param") else torch.int32,
+                           pin_memory=True) for k in small}
+    rng = np.random.default_rng(args.seed + rank)
+    S = max(0, args.cpu_sample) if world == 1 else 0
+    samp = np.sort(rng.choice(N, size=min(S, N), replace=False)) if S else np.zeros(0, int)
+    pport = torch.empty((max(len(samp), 1), nchan, nbin), dtype=torch.float64, pin_memory=True)
+    stream = eng.stream
+    cstream = torch.cuda.Stream(dev)
+    ev = []
+
+    def run(record):
+        copied = [None] * len(starts)  # (start, end) events of each chunk's copy
+        freed = [None] * len(starts)   # each chunk's unpack done: its raw buffer is free
+
+        def copy(ci):
+            s0 = starts[ci]
+            n = min(C, N - s0)
+            b = ci % nb
+            if ci >= nb:
+                cstream.wait_event(freed[ci - nb])
+            a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            with torch.cuda.stream(cstream):
+                a.record(cstream)
+                draw[b][:n].copy_(hraw[ci], non_blocking=True)
+                dscl[b][:n].copy_(hscl[s0:s0 + n], non_blocking=True)
+                doff[b][:n].copy_(hoff[s0:s0 + n], non_blocking=True)
+                e.record(cstream)
+            copied[ci] = (a, e)
+
+        copy(0)
+        for ci, s0 in enumerate(starts):
+            n = min(C, N - s0)
+            b = ci % nb
+            stream.wait_event(copied[ci][1])
+            u0, u1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+            u0.record(stream)
+            eng.unpack_subints(draw[b][:n], dscl[b][:n], doff[b][:n], 0, out=fbuf[:n])
+            u1.record(stream)
+            freed[ci] = u1
+            if ci + 1 < len(starts):
+                copy(ci + 1)
+            out = eng.fit_batch(fbuf[:n, 0], model, freqs, P[:n], init[:n], flags,
+                                nu_fit=nu[:n], guess=True, guess_Ns=100)
+            e2.record(stream)
+            with torch.cuda.stream(stream):
+                for k in small:
+                    host[k][s0:s0 + n].copy_(out[k], non_blocking=True)
+                if record:
+                    for j in np.flatnonzero((samp >= s0) & (samp < s0 + n)):
+                        pport[j].copy_(fbuf[int(samp[j]) - s0, 0], non_blocking=True)
+            if record:
+                ev.append((copied[ci][0], copied[ci][1], u0, u1, e2))
+        torch.cuda.synchronize()
+
+    # warm-up: one chunk's copy, unpack and fit (workspace, allocator, kernels)
+    n0 = min(C, N)
+    draw[0][:n0].copy_(hraw[0])
+    dscl[0][:n0].copy_(hscl[:n0])
+    doff[0][:n0].copy_(hoff[:n0])
+    eng.unpack_subints(draw[0][:n0], dscl[0][:n0], doff[0][:n0], 0, out=fbuf[:n0])
+    eng.fit_batch(fbuf[:n0, 0], model, freqs, P[:n0], init[:n0], flags, nu_fit=nu[:n0],
+                  guess=True, guess_Ns=100)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(True)
+    if world > 1:
+        torch.distributed.barrier()
+    t1 = time.perf_counter()
+    elapsed, rank_times = dist_times(t1 - t0, world, dev)
+    copy_ms = sum(a.elapsed_time(b) for a, b, _, _, _ in ev)
+    unpack_ms = sum(c.elapsed_time(d) for _, _, c, d, _ in ev)
+    fit_ms = sum(d.elapsed_time(e) for _, _, _, d, e in ev)
+    raw_bytes = N * nchan * nbin * 2 + 2 * N * nchan * 8
+    status = host["status"].numpy()
+    nfev = host["nfev"].numpy()
+    del draw, fbuf, hraw
+    if rank != 0:
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
+    parity = None
+    if len(samp):
+        import multiprocessing as mp
+        jobs = [(pport[j].numpy().copy(), nchan, nbin, args.seed, flags) for j in range(len(samp))]
+        with mp.get_context("spawn").Pool(min(16, len(jobs))) as pool:
+            refs = pool.map(_oracle_fit, jobs)
+        hp = host["params"].numpy()
+        gaps = {nm: float(max(abs(hp[i, j] - r[0][j]) / r[1][j] for i, r in zip(samp, refs)))
+                for j, nm in enumerate(["phi", "DM", "GM"])}
+        parity = {"sample": len(samp), "subints": [int(i) for i in samp],
+                  "tolerance": "1e-3 sigma (north_star)", "max_over_sigma": gaps,
+                  "status_match": bool(all(status[i] == r[2] for i, r in zip(samp, refs))),
+                  "oracle_input": "the dequantised samples the device fitted"}
+    line = {
+        "metric": "TOAs/sec (config 4 per-GPU shard from host memory, phase+DM+GM, "
+                  "128ch x 2048bin fp64)",
+        "value": round(N * world / elapsed, 2), "unit": "TOAs/s", "n_gpus": world, "steps": 1,
+        "warmup": 1, "ms_per_step": round(elapsed * 1e3, 3),
+        "rank_ms_per_step": [round(t * 1e3, 3) for t in rank_times],
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic int16 PSRFITS-style samples (DATA, DAT_SCL, DAT_OFFS) resident in "
+                "pinned host memory; PCIe copies inside the timed region",
+        "config": {"workload": desc, "nsub_per_gpu": N, "chunk_subints": C, "chunks": len(starts),
+                   "nchan": nchan, "nbin": nbin, "fit_flags": flags, "guess_Ns": 100,
+                   "host_input_gb_per_gpu": round(raw_bytes / 1e9, 2),
+                   "parallelism": "subint-sharded dp%d" % world},
+        "pcie_h2d_gbs": round(raw_bytes / (copy_ms / 1e3) / 1e9, 2),
+        "pcie_bound_value": round(N / (copy_ms / 1e3), 2),
+        "copy_ms": round(copy_ms, 2), "unpack_ms": round(unpack_ms, 2), "fit_ms": round(fit_ms, 2),
+        "overlap": "chunk i + 1 copied on a second queue while chunk i is unpacked and fitted "
+                   "(two device buffers); copy_ms / unpack_ms / fit_ms are each side's own "
+                   "event time",
+        "fit_only_value": round(N / (fit_ms / 1e3), 2),
+        "per_toa_us": round(elapsed / N * 1e6, 4),
+        "status_counts": {str(k): int(v) for k, v in zip(*np.unique(status, return_counts=True))},
+        "mean_nfev": float(np.mean(nfev)), "parity_sample": parity,
+    }
+    print(json.dumps(line))
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
 def main_get_toas(args, eng, rank, world, w, data, step, desc):
     """--config get_toas: value = GetTOAs.get_TOAs TOAs/s on a registered
     archive of the bench's subints (device-resident), .tim text included."""
@@ -886,23 +1092,13 @@ def main_get_toas(args, eng, rank, world, w, data, step, desc):
     print(json.dumps(line))
 
 
-def main_ppalign(args, eng, rank, world):
-    """--config ppalign: value = archive-iterations/s of align_archives at
-    config 5 (4096 x 256 x 2048, niter 3)."""
-    if world > 1:
-        raise SystemExit("--config ppalign runs on one GPU here; align_archives shards its "
-                         "units and all-reduces when torch.distributed is initialised")
-    from pulseportraiture_amd import ppalign
-    narch = args.nsub or args.ppalign_narch
-    if args.no_spec_cache:
-        ppalign.SPEC_CACHE = False
-    cache = ppalign.SPEC_CACHE
-    r = leg_ppalign(eng, narch, args.ppalign_niter, args.seed)
-    kt = r.pop("_ktimes")
-    r["spec_cache"] = cache
+def ppalign_roofline(kt, narch, niter, cache):
+    """Roofline of one align_archives call at config 5's shape from its
+    per-kernel HIP-event times kt ({kernel: (ms, launches)}): the dominant
+    kernel's achieved HBM rate on its algorithmic bytes, the PMC traffic of
+    the same kernel (profiles/, per call), the others beside it."""
     nchan, nbin = 256, 2048
     nharm = nbin // 2 + 1
-    niter = args.ppalign_niter
     # algorithmic bytes of one align_archives call, per kernel.  With the
     # data-spectrum cache the data pass runs in the first iteration only
     # (reads every sample, writes the spectra D), the moment passes read D
@@ -953,6 +1149,24 @@ def main_ppalign(args, eng, rank, world):
         src = PMC_TRAFFIC["ppalign"]
         roof["traffic_source"] = os.path.relpath(src, ROOT) if roof["traffic"] else None
         roof["other_kernels"] = {k: v for k, v in kernels.items() if k != dom}
+    return roof
+
+
+def main_ppalign(args, eng, rank, world):
+    """--config ppalign: value = archive-iterations/s of align_archives at
+    config 5 (4096 x 256 x 2048, niter 3)."""
+    if world > 1:
+        raise SystemExit("--config ppalign runs on one GPU here; align_archives shards its "
+                         "units and all-reduces when torch.distributed is initialised")
+    from pulseportraiture_amd import ppalign
+    narch = args.nsub or args.ppalign_narch
+    if args.no_spec_cache:
+        ppalign.SPEC_CACHE = False
+    cache = ppalign.SPEC_CACHE
+    r = leg_ppalign(eng, narch, args.ppalign_niter, args.seed)
+    kt = r.pop("_ktimes")
+    r["spec_cache"] = cache
+    roof = ppalign_roofline(kt, narch, args.ppalign_niter, cache)
     line = {"metric": "archive-iterations/sec (ppalign.align_archives, 256ch×2048bin fp64)",
             "value": r["value"], "unit": r["unit"], "n_gpus": 1, "steps": 1, "warmup": 1,
             "ms_per_step": round(r["s_per_call"] * 1e3, 2), "higher_is_better": True,

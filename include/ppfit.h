@@ -44,7 +44,14 @@
  *    trust-ncg codes (0 gradient small / NaN, 1 maxiter, 2 no predicted
  *    reduction, 3 linalg error), as returned by the reference's
  *    results.status (pptoaslib.py:1018).
- *  - nbin must be a power of two in [64, 8192]; nchan <= PPF_MAX_NCHAN.
+ *  - Shapes the reference accepts and this library refuses (PPF_ERR_INVALID
+ *    with a message, never a silent fallback): nbin must be a power of two
+ *    in [64, 8192] (the register / LDS FFTs and the Taylor power tables are
+ *    built per power of two; the reference's numpy rfft takes any length,
+ *    pptoaslib.py:976-978), and nchan <= PPF_MAX_NCHAN (the per-channel
+ *    metadata of a subint is staged in LDS; the reference takes any channel
+ *    count).  A caller with other shapes must resample (nbin) or split the
+ *    channels itself; there is no generic-length path.
  */
 #ifndef PPFIT_H
 #define PPFIT_H

@@ -137,6 +137,30 @@ int twiddles(ppf_ctx* ctx, int nbin, const double2** out) {
 
 void launch_fit_taylor(const ppf_ctx* ctx, dim3 g, size_t lds, hipStream_t st, const FitArgs& fa);
 
+// Moments per channel of T slot 0 that k_fit_taylor's LDS copy holds:
+// kTaylorBlocksPerCU blocks of (static LDS + Meta + nchan * tnl doubles) in a
+// CU's LDS, whole KB per block.
+int taylor_lds_moments(int nchan, size_t lds_meta) {
+  static size_t stat = 0;
+  if (!stat) {
+    size_t mx = 0;
+    const void* ks[4] = {reinterpret_cast<const void*>(&k_fit_taylor<true, false>),
+                         reinterpret_cast<const void*>(&k_fit_taylor<false, false>),
+                         reinterpret_cast<const void*>(&k_fit_taylor<true, true>),
+                         reinterpret_cast<const void*>(&k_fit_taylor<false, true>)};
+    for (const void* k : ks) {
+      hipFuncAttributes at;
+      if (hipFuncGetAttributes(&at, k) != hipSuccess) return 0;
+      mx = std::max(mx, at.sharedSizeBytes);
+    }
+    stat = mx;
+  }
+  const size_t per_block = (kLdsPerCU / kTaylorBlocksPerCU) & ~(size_t)1023;
+  if (per_block <= stat + lds_meta) return 0;
+  const size_t nl = (per_block - stat - lds_meta) / ((size_t)nchan * sizeof(double));
+  return (int)std::min<size_t>(nl, kMT);
+}
+
 int vpow_table(ppf_ctx* ctx, int nbin, const double2** out) {
   const int l = ilog2_exact(nbin);
   if (!ctx->vp[l]) {
@@ -451,7 +475,7 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
 
   // per-subint workspace layout
   const size_t bX = (size_t)nchan * NHP * sizeof(double2);
-  const size_t bT = taylor ? (size_t)2 * nchan * kMT * sizeof(double2) : 0;
+  const size_t bT = taylor ? (size_t)2 * nchan * kMT * sizeof(double) : 0;
   const size_t bR = (size_t)NHP * sizeof(double2);
   const size_t bC = (size_t)nchan * sizeof(double);
   const size_t bAcc = (size_t)2 * nchan * 10 * sizeof(double);
@@ -538,7 +562,7 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   fa.st = reinterpret_cast<SolveState*>(base + offSt);
   fa.acc = reinterpret_cast<double*>(base + offAcc);
   fa.wsc = reinterpret_cast<double*>(base + offW);
-  fa.T = taylor ? reinterpret_cast<double2*>(base + offT) : nullptr;
+  fa.T = taylor ? reinterpret_cast<double*>(base + offT) : nullptr;
   fa.tw = tw;
   fa.vpow = nullptr;
   if (taylor)
@@ -566,10 +590,11 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   fa.o_hess = o->hess;
 
   const size_t lds_meta = align256((size_t)nchan * (5 * sizeof(double) + sizeof(int)));
-  // k_fit_taylor keeps T slot 0 in LDS when it fits (kTaylorLds)
-  const size_t tl_bytes = (size_t)nchan * kMT * sizeof(double2);
-  fa.tlds = (taylor && tl_bytes <= kTaylorLds) ? (int)lds_meta : 0;
-  const size_t lds_taylor = lds_meta + (fa.tlds ? tl_bytes : 0);
+  // k_fit_taylor keeps moments [0, tnl) of T slot 0 in LDS (all of them when
+  // they fit beside kTaylorBlocksPerCU - 1 other blocks)
+  fa.tnl = taylor ? taylor_lds_moments(nchan, lds_meta) : 0;
+  fa.tlds = fa.tnl > 0 ? (int)lds_meta : 0;
+  const size_t lds_taylor = lds_meta + (size_t)nchan * fa.tnl * sizeof(double);
   // trust-ncg scattering fits: every evaluation split over blocks of >= 64
   // fitted channels (k_scat_sweep / k_scat_step)
   // (PPF_OPT_SCAT_SPLIT = 0: one block per subint, k_solve<true>)

@@ -511,11 +511,14 @@ __constant__ double c_inv_fact[kMT] = {
     3.279889237069838e-30, 1.1309962886447718e-31, 3.7699876288159054e-33, 1.2161250415535181e-34};
 
 struct TaylorSrc {
-  const double2* T;    // this subint's moment rows for one centre: [nchan][kMT], or null (exact)
+  const double* T;     // this subint's compact moment rows for one centre: [nchan][kMT],
+                       // or null (exact sweeps)
   const double* xc;    // centre params
   const double* refc;  // centre reference frequencies
   bool same = false;   // evaluation refs == refc: offsets from Meta d1/d2
   const double* ifact = nullptr;  // LDS copy of c_inv_fact, or null (constant memory)
+  const double* Tl = nullptr;     // LDS copy of moments [0, nl) of these rows: [nchan][nl]
+  int nl = 0;
 };
 
 // offset from the centre for evaluation refs == centre refs:
@@ -533,37 +536,47 @@ __device__ __forceinline__ double taylor_delta(const double* prm, const double* 
   return d - rint(d);
 }
 
-__device__ __forceinline__ void taylor_cells(const double2* __restrict__ Tn, int h, double d,
-                                             double Ks, const double* ifact, double* acc) {
+// Channel n's series G_j = sum_m T_{m+j} (i y)^m / m! (j = 0, 1, 2), this
+// lane's terms m = h + 8 q.  i^m = i^h for every m of the lane (m = h mod 4),
+// so of G_0, G_1, G_2 only Re G_0, Im G_1, Re G_2 are formed, and each reads
+// one real part per moment: Re(i^m T_{m+j}) or Im(...) is +-Re T_{m+j} when
+// m + j is even and +-Im T_{m+j} when it is odd -- the compact moment
+// (kMT doubles per channel).  The lane's sums are those of the complex
+// series' selected parts, operation for operation.
+__device__ __forceinline__ void taylor_cells(const TaylorSrc& ts, int n, int h, double d,
+                                             double Ks, double* acc) {
   // 1/m! by lane-varying m: from LDS when the caller staged it (a constant-
   // memory gather costs a memory round trip per call)
-  const double* fz = ifact ? ifact : c_inv_fact;
+  const double* fz = ts.ifact ? ts.ifact : c_inv_fact;
+  const double* __restrict__ Tg = ts.T + (size_t)n * kMT;
+  const double* __restrict__ Tl = ts.Tl + (size_t)n * ts.nl;
+  const int nl = ts.nl;
+  // moment i of the channel: the LDS copy below nl, the HBM rows above
+  auto tm = [&](int i) { return i < nl ? Tl[i] : Tg[i]; };
   const double y = kTwoPi * Ks * d;
   double yh = 1.0;
   for (int i = 0; i < h; ++i) yh *= y;
   const double y2 = y * y, y4 = y2 * y2, y8 = y4 * y4;
-  double2 S0 = cmk(0.0, 0.0), S1 = S0, S2 = S0;
+  double S0 = 0.0, S1 = 0.0, S2 = 0.0;
   double ym = yh;
 #pragma unroll
   for (int q = 0; q < (kMTerm + 7) / 8; ++q) {
     const int m = h + 8 * q;
     if (m < kMTerm) {  // T up to index kMTerm + 1 = kMT - 1
       const double cf = ym * fz[m];
-      const double2 t0 = Tn[m], t1 = Tn[m + 1], t2 = Tn[m + 2];
-      S0 = cmk(fma(cf, t0.x, S0.x), fma(cf, t0.y, S0.y));
-      S1 = cmk(fma(cf, t1.x, S1.x), fma(cf, t1.y, S1.y));
-      S2 = cmk(fma(cf, t2.x, S2.x), fma(cf, t2.y, S2.y));
+      S0 = fma(cf, tm(m), S0);
+      S1 = fma(cf, tm(m + 1), S1);
+      S2 = fma(cf, tm(m + 2), S2);
     }
     ym *= y8;
   }
-  // i^m = i^h for every m of this lane (m = h mod 4): only the parts the
-  // sweep needs, Re G_0, Im G_1, Re G_2
+  // the signs of i^h: Re G_0 (part of T_m), Im G_1 (T_{m+1}), Re G_2 (T_{m+2})
   double r0, i1, r2;
   switch (h & 3) {
-    case 1: r0 = -S0.y; i1 = S1.x; r2 = -S2.y; break;
-    case 2: r0 = -S0.x; i1 = -S1.y; r2 = -S2.x; break;
-    case 3: r0 = S0.y; i1 = -S1.x; r2 = S2.y; break;
-    default: r0 = S0.x; i1 = S1.y; r2 = S2.x; break;
+    case 1: r0 = -S0; i1 = S1; r2 = -S2; break;
+    case 2: r0 = -S0; i1 = -S1; r2 = -S2; break;
+    case 3: r0 = S0; i1 = -S1; r2 = S2; break;
+    default: r0 = S0; i1 = S1; r2 = S2; break;
   }
   acc[0] = r0;
   acc[1] = Ks * i1;
@@ -623,8 +636,8 @@ __device__ __forceinline__ void sweep_taylor0(const FitArgs& a, const Meta& m, c
       const int j = (gi + u * kWaves) * 8 + g8;
       const int jj = j < m.nok ? j : m.nok - 1;
       double acc[NACC];
-      taylor_cells(ts.T + (size_t)m.chan[jj] * kMT, h,
-                   taylor_delta_lin(prm, ts.xc, m.d1[jj], m.d2[jj]), Ks, ts.ifact, acc);
+      taylor_cells(ts, m.chan[jj], h, taylor_delta_lin(prm, ts.xc, m.d1[jj], m.d2[jj]), Ks,
+                   acc);
 #pragma unroll
       for (int i = 0; i < 3; ++i) sg[u][i] = group8_sum(acc[i]);
     }
@@ -735,7 +748,7 @@ __device__ __forceinline__ void sweep(const FitArgs& a, const Meta& m, int c, in
     if (!SCAT && ts.T) {
       const double dl = ts.same ? taylor_delta_lin(prm, ts.xc, m.d1[jj], m.d2[jj])
                                 : taylor_delta(prm, refs, ts, fr, P);
-      taylor_cells(ts.T + (size_t)n * kMT, h, dl, 0.5 * (double)a.nbin, ts.ifact, acc);
+      taylor_cells(ts, n, h, dl, 0.5 * (double)a.nbin, acc);
     } else if (!scat) {
       const double phif = phase_frac(prm, fr, refs, P);
       const double2* Xr = a.X + ((size_t)c * a.nchan + n) * a.NHP;

@@ -54,17 +54,19 @@ struct PhaseShiftArgs {
 // evaluation at per-channel offset y = 2 pi N delta uses terms m < kMTerm and
 // is accepted while |y| <= kTaylorY, where the truncation
 // kTaylorY^kMTerm / kMTerm! e^kTaylorY is < 2e-17 of sum_k |W_k|.
+// Only one real part of each moment is ever used (Re T_m for even m, Im T_m
+// for odd m: the sweep needs Re G_0, Im G_1, Re G_2 and i^m selects that part),
+// so a channel's moments are kMT doubles ("compact moments", taylor_cells).
 constexpr int kMT = 32;
 // rows of the moment power table: every harmonic a moment block can touch
 // (k <= N plus the zero-padded tail of the last block of steps)
 __host__ __device__ constexpr int kVpowRows(int N) { return N + 1 + 4 * 64; }
 constexpr int kMTerm = kMT - 2;
-// largest LDS copy of one T slot k_fit_taylor keeps (48 KB: nchan <= 96), so
-// that two of its blocks (the register limit) still fit a CU's 160 KB of LDS
-#ifndef PPF_TAYLOR_LDS_KB
-#define PPF_TAYLOR_LDS_KB 48
-#endif
-constexpr size_t kTaylorLds = PPF_TAYLOR_LDS_KB * 1024;
+// k_fit_taylor keeps moments [0, tnl) of T slot 0 in LDS, tnl as large as
+// lets kTaylorBlocksPerCU of its blocks share a CU's kLdsPerCU (the register
+// limit is the same three blocks): all kMT up to 128 channels, 16 at 256
+constexpr size_t kLdsPerCU = 160 * 1024;
+constexpr int kTaylorBlocksPerCU = 3;
 constexpr double kTaylorY = 3.0;
 
 // Per-subint solver state handed from k_guess -> k_solve -> k_post (global).
@@ -112,11 +114,12 @@ struct FitArgs {
   const double* guess_nu;    // [nsub] or null
   const double* guess_tau;   // [nsub] or null
   SolveState* st;            // chunk [c]
-  double2* T;                // chunk [c][2][nchan][kMT] Taylor moments
+  double* T;                 // chunk [c][2][nchan][kMT] compact Taylor moments
   int tlds;                  // k_fit_taylor: byte offset of its LDS copy of T slot 0 in
                              // dynamic LDS (after the Meta arrays), 0 = read T from HBM
+  int tnl;                   //   moments [0, tnl) of each channel in that copy: [nchan][tnl]
   const double2* tw;         // rfft twiddles e^{-2 pi i m / nbin}
-  const double2* vpow;       // [kVpowRows(N)][16] (v^col, v^(16+col)), v = k / N
+  const double2* vpow;       // [kVpowRows(N)][16] (v^(2 col), v^(2 col + 1)), v = k / N
   const double2* Mmean;      // [nmodel][NHP] mean template spectrum or null
   unsigned long long* ptime; // [PPF_PHASE_N] k_fit_taylor phase clocks, or null
   double* trace;             // solver trace (ppf_set_trace): [nsub][trace_cap][kTraceRec]

@@ -67,12 +67,14 @@ __device__ __forceinline__ void rs_swap(const double* v, double* out) {
 //   T_nm = sum_k v_k^m W_nk,  v_k = k / N,  W_nk = X_nk e^{2 pi i k phi_c,n}.
 // The k-contraction runs on the f64 matrix cores: each wave takes tiles of 16
 // fitted channels; per step of 4 harmonics, v_mfma_f64_16x16x4 multiplies
-// A = v^m (16 moments x 4 harmonics) by B = Re W and by B = Im W (4 harmonics
-// x 16 channels) into accumulators for moments 0-15 and 16-31.  Lane l
-// supplies harmonic 4 s + (l >> 4) of channel l & 15 to B and v^(l & 15),
-// v^(16 + (l & 15)) of that harmonic to A (v is exact since N is a power of
-// two).  X rows stream through registers U steps ahead of the MFMAs.  All kMT moments are
-// kept (cnt = kMT): the truncation bound then holds for any spectrum.
+// A = v^(2i) (the 16 even moments x 4 harmonics) by B = Re W, and A = v^(2i+1)
+// (the 16 odd moments) by B = Im W (4 harmonics x 16 channels): the compact
+// moments (kernels.hpp), Re T_m for even m and Im T_m for odd m, and nothing
+// else -- two MFMAs per step.  Lane l supplies harmonic 4 s + (l >> 4) of
+// channel l & 15 to B and v^(2 (l & 15)), v^(2 (l & 15) + 1) of that harmonic
+// to A (v is exact since N is a power of two).  X rows stream through
+// registers U steps ahead of the MFMAs.  All kMT moments are kept (cnt =
+// kMT): the truncation bound then holds for any spectrum.
 // ---------------------------------------------------------------------------
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
@@ -86,24 +88,28 @@ constexpr int kMomReseedSteps = 8;
 // X rows: plain loads (the non-temporal hint measured slower here)
 __device__ __forceinline__ double2 xload(const double2* p) { return *p; }
 
-// v^col and v^(16+col) of harmonic k (v = k iN), in the table's fixed order.
+// v^m (m < 32) in one fixed order: v, v^2, v^4, v^8 by squaring, the
+// factors of m & 15 multiplied in bit order, then v^16 = v^8 v^8 for m >= 16.
+__device__ __forceinline__ double vpow_m(double v, double v2, double v4, double v8, int m) {
+  double pc = (m & 1) ? v : 1.0;
+  pc *= (m & 2) ? v2 : 1.0;
+  pc *= (m & 4) ? v4 : 1.0;
+  pc *= (m & 8) ? v8 : 1.0;
+  return (m & 16) ? pc * (v8 * v8) : pc;
+}
+
+// v^(2 col) and v^(2 col + 1) of harmonic k (v = k iN), in the table's order.
 __device__ __forceinline__ double2 vpow_inline(int k, double iN, int col) {
   const double v = (double)k * iN;
   const double v2 = v * v, v4 = v2 * v2, v8 = v4 * v4;
-  double pc = (col & 1) ? v : 1.0;
-  pc *= (col & 2) ? v2 : 1.0;
-  pc *= (col & 4) ? v4 : 1.0;
-  pc *= (col & 8) ? v8 : 1.0;
-  return cmk(pc, pc * (v8 * v8));
+  return cmk(vpow_m(v, v2, v4, v8, 2 * col), vpow_m(v, v2, v4, v8, 2 * col + 1));
 }
 
-// The A operand, v^m for the harmonic k = 4 step + (l >> 4) of a lane and
-// its moment rows m = l & 15 and 16 + (l & 15), comes from a table built once
-// per nbin (k_vpow): the powers are the same for every channel, so forming
-// them per step (3 squarings, 4 selected products and 2 more for v^16+m, on
-// every lane) would cost more vector issue than the two MFMAs they feed.
-// Entries are formed in one fixed order: v, v^2, v^4, v^8 by squaring, the
-// factors of m multiplied in bit order, v^(16+m) = v^m (v^8 v^8).
+// The A operands, v^(2i) and v^(2i+1) for the harmonic k = 4 step + (l >> 4)
+// of a lane and its row i = l & 15, come from a table built once per nbin
+// (k_vpow): the powers are the same for every channel, so forming them per
+// step (3 squarings and up to 5 selected products each, on every lane) would
+// cost more vector issue than the two MFMAs they feed.
 __global__ void k_vpow(double2* vp, int N, int rows) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= rows * 16) return;
@@ -113,9 +119,9 @@ __global__ void k_vpow(double2* vp, int N, int rows) {
 
 // One 16-channel tile by one wave: lane l handles channel n (column l & 15 of
 // the B operand; ok = fitted) at harmonic offset l >> 4, with centre phase
-// phic; U = steps in flight.  Each step is four MFMAs: re and im parts of W
-// (two B matrices, 16 channels each) times the moment rows 0-15 and 16-31 of
-// A, with even and odd steps in separate accumulators (independent chains).
+// phic; U = steps in flight.  Each step is two MFMAs: Re W times the even
+// moment rows of A and Im W times the odd ones, with even and odd steps in
+// separate accumulators (independent chains).
 // A lane rotates its own element and feeds it straight to the matrix core:
 // no cross-lane trade, no select.  Its two phasor chains (even / odd steps)
 // restart from turn_phasor every kMomReseedSteps steps.  The next block's X and power rows
@@ -145,9 +151,9 @@ __device__ __forceinline__ void moment_tile16(const FitArgs& a, int c, int slot,
   // power row of step t for this lane: vpow[(4 t + kk) * 16 + col]
   const double2* __restrict__ vp = a.vpow + (size_t)kk * 16 + col;
   const double2 s8 = turn_phasor(8.0, phic);
-  // re (d) and im (g) parts; moments 0-15 / 16-31; even / odd steps
-  f64x4 d0 = {0.0, 0.0, 0.0, 0.0}, d1 = d0, d2 = d0, d3 = d0;
-  f64x4 g0 = d0, g1 = d0, g2 = d0, g3 = d0;
+  // Re T of the even moments (d) and Im T of the odd ones (g); even / odd steps
+  f64x4 d0 = {0.0, 0.0, 0.0, 0.0}, d2 = d0;
+  f64x4 g0 = d0, g2 = d0;
   // loads are unpredicated (X index clamped to N; the power table is padded
   // past the last block); cells k > N and idle lanes are zeroed at use
   double2 xb[U], pb[U], mb[DSP ? U : 1];
@@ -179,13 +185,9 @@ __device__ __forceinline__ void moment_tile16(const FitArgs& a, int c, int slot,
       const double2 W1 = cmul(xcell(b * U + 2 * u + 1, 2 * u + 1), e1);
       const double2 p0 = pb[2 * u], p1 = pb[2 * u + 1];
       d0 = __builtin_amdgcn_mfma_f64_16x16x4f64(p0.x, W0.x, d0, 0, 0, 0);
-      d1 = __builtin_amdgcn_mfma_f64_16x16x4f64(p0.y, W0.x, d1, 0, 0, 0);
-      g0 = __builtin_amdgcn_mfma_f64_16x16x4f64(p0.x, W0.y, g0, 0, 0, 0);
-      g1 = __builtin_amdgcn_mfma_f64_16x16x4f64(p0.y, W0.y, g1, 0, 0, 0);
+      g0 = __builtin_amdgcn_mfma_f64_16x16x4f64(p0.y, W0.y, g0, 0, 0, 0);
       d2 = __builtin_amdgcn_mfma_f64_16x16x4f64(p1.x, W1.x, d2, 0, 0, 0);
-      d3 = __builtin_amdgcn_mfma_f64_16x16x4f64(p1.y, W1.x, d3, 0, 0, 0);
-      g2 = __builtin_amdgcn_mfma_f64_16x16x4f64(p1.x, W1.y, g2, 0, 0, 0);
-      g3 = __builtin_amdgcn_mfma_f64_16x16x4f64(p1.y, W1.y, g3, 0, 0, 0);
+      g2 = __builtin_amdgcn_mfma_f64_16x16x4f64(p1.y, W1.y, g2, 0, 0, 0);
       e0 = cmul(e0, s8);
       e1 = cmul(e1, s8);
       // rolling prefetch: this pair's registers take the next block's rows
@@ -199,17 +201,12 @@ __device__ __forceinline__ void moment_tile16(const FitArgs& a, int c, int slot,
     }
   }
   d0 += d2;
-  d1 += d3;
   g0 += g2;
-  g1 += g3;
-  // D[row = moment (l >> 4) + 4 r][col = channel l & 15]
+  // D[row i = (l >> 4) + 4 r][col = channel l & 15]: moments 2 i and 2 i + 1
   if (ok) {
-    double2* Tn = a.T + (((size_t)c * 2 + slot) * a.nchan + n) * kMT;
+    double2* Tn = reinterpret_cast<double2*>(a.T + (((size_t)c * 2 + slot) * a.nchan + n) * kMT);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      Tn[kk + 4 * r] = cmk(d0[r], g0[r]);
-      Tn[16 + kk + 4 * r] = cmk(d1[r], g1[r]);
-    }
+    for (int r = 0; r < 4; ++r) Tn[kk + 4 * r] = cmk(d0[r], g0[r]);
   }
 }
 
@@ -218,8 +215,10 @@ __device__ __forceinline__ void moment_tile16(const FitArgs& a, int c, int slot,
 // channel (l & 15) >> 1, part p = l & 1; steps go in pairs, lane part p
 // loads X at the harmonic of step 2u + p and rotates it on its own phasor
 // chain (the p chain of moment_tile16), keeps the part it feeds to B and
-// trades the other with its partner (DPP quad_perm [1,0,3,2]).  Powers are
-// formed inline in the table's order, and every MFMA sees the operands of
+// trades the other with its partner (DPP quad_perm [1,0,3,2]).  B's columns
+// are (channel, Re W) and (channel, Im W): the even-row MFMA's Re columns and
+// the odd-row MFMA's Im columns are the compact moments.  Powers are formed
+// inline in the table's order, and every kept element sees the operands of
 // moment_tile16: bitwise the same moments.  DSP: as moment_tile16's.
 template <int U, bool DSP>
 __device__ __forceinline__ void moment_tile8(const FitArgs& a, int c, int slot, int n, bool ok,
@@ -276,14 +275,12 @@ __device__ __forceinline__ void moment_tile8(const FitArgs& a, int c, int slot, 
   }
   d0 += d2;
   d1 += d3;
-  // D[row = moment (l >> 4) + 4 r][col = l & 15]
+  // D[row i = (l >> 4) + 4 r][col = l & 15]: the Re lanes (part 0) keep the
+  // even moment 2 i from d0, the Im lanes (part 1) the odd one 2 i + 1 from d1
   if (ok) {
-    double* Tn = reinterpret_cast<double*>(a.T + (((size_t)c * 2 + slot) * a.nchan + n) * kMT);
+    double* Tn = a.T + (((size_t)c * 2 + slot) * a.nchan + n) * kMT;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      Tn[2 * (kk + 4 * r) + part] = d0[r];
-      Tn[2 * (16 + kk + 4 * r) + part] = d1[r];
-    }
+    for (int r = 0; r < 4; ++r) Tn[2 * (kk + 4 * r) + part] = part ? d1[r] : d0[r];
   }
 }
 
@@ -351,18 +348,20 @@ struct TaylorShared {
   int sv_hits, sv_k, sv_status, sv_nfev;
 };
 
-// T slot 0 of subint c into the kernel's LDS copy (all threads; the caller
-// syncs): nchan * kMT entries, kU loads in flight per thread.
-__device__ __forceinline__ void stage_T0(const FitArgs& a, int c, double2* tl) {
-  const double2* __restrict__ src = a.T + (size_t)c * 2 * a.nchan * kMT;
-  const int n = a.nchan * kMT;
+// Moments [0, a.tnl) of T slot 0 of subint c into the kernel's LDS copy
+// [nchan][tnl] (all threads; the caller syncs), kU loads in flight per thread.
+__device__ __forceinline__ void stage_T0(const FitArgs& a, int c, double* tl) {
+  const double* __restrict__ src = a.T + (size_t)c * 2 * a.nchan * kMT;
+  const int nl = a.tnl;
+  const int n = a.nchan * nl;
   constexpr int kU = 8;
   for (int i0 = 0; i0 < n; i0 += kBlock * kU) {
-    double2 v[kU];
+    double v[kU];
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const int i = i0 + u * kBlock + (int)threadIdx.x;
-      v[u] = i < n ? src[i] : cmk(0.0, 0.0);
+      const int ch = i / nl;
+      v[u] = i < n ? src[(size_t)ch * kMT + (i - ch * nl)] : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
@@ -430,7 +429,7 @@ __global__ __launch_bounds__(kBlock, 3) void k_fit_taylor(FitArgs a) {
   SolveState& st = a.st[c];
   // T slot 0 (k_moments) read once into LDS: every sweep about centre 0 then
   // reads LDS instead of HBM.  load_meta's barrier publishes it.
-  double2* tl = a.tlds ? reinterpret_cast<double2*>(dyn + a.tlds) : nullptr;
+  double* tl = a.tlds ? reinterpret_cast<double*>(dyn + a.tlds) : nullptr;
   if (tl) stage_T0(a, c, tl);
   const Meta m = load_meta(a, c, s, dmeta, &sh.nok);
   const double P = a.P[s];
@@ -510,8 +509,9 @@ __global__ __launch_bounds__(kBlock, 3) void k_fit_taylor(FitArgs a) {
     return best;
   };
   auto source = [&](int q) {
-    return TaylorSrc{(q == 0 && tl) ? tl : a.T + ((size_t)c * 2 + q) * a.nchan * kMT, sh.xc[q],
-                     refs, true, sh.ifact};
+    const bool l = q == 0 && tl;
+    return TaylorSrc{a.T + ((size_t)c * 2 + q) * a.nchan * kMT, sh.xc[q], refs, true, sh.ifact,
+                     l ? tl : nullptr, l ? a.tnl : 0};
   };
   // no stored centre covers p: p itself becomes one (one more X pass)
   auto recentre = [&](const double* p) -> int {

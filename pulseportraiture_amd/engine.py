@@ -786,6 +786,27 @@ class Engine:
                                                       _ptr(ph), _ptr(w), _ptr(accum)))
         return (cache, ph, w)
 
+    def unpack_subints(self, raw, scl, offs, pmode=0, out=None):
+        """PSRFITS samples to values on the device (ppf_unpack_subints):
+        raw [nsub, npol, nchan, nbin] uint8 / int16 / float32 device tensor,
+        scl / offs [nsub, npol, nchan] (DAT_SCL, DAT_OFFS); out [nsub, npo,
+        nchan, nbin] float64, npo = 1 when pmode pscrunches."""
+        rt = {torch.uint8: 1, torch.int16: 2, torch.float32: 3}[raw.dtype]
+        nsub, npol, nchan, nbin = raw.shape
+        npo = 1 if pmode else npol
+        if out is None:
+            out = torch.empty((nsub, npo, nchan, nbin), dtype=torch.float64, device=self.device)
+        for t in (raw, scl, offs, out):
+            if t.device != self.device or not t.is_contiguous():
+                raise PPFitError("unpack_subints: contiguous tensors on %s" % self.device)
+        if tuple(scl.shape) != (nsub, npol, nchan) or tuple(offs.shape) != (nsub, npol, nchan) \
+                or tuple(out.shape) != (nsub, npo, nchan, nbin) or out.dtype != torch.float64 \
+                or scl.dtype != torch.float64 or offs.dtype != torch.float64:
+            raise PPFitError("unpack_subints: shapes / dtypes do not match raw")
+        self._chk(self.lib.ppf_unpack_subints(self.ctx, nsub, npol, nchan, nbin, rt, _ptr(raw),
+                                              _ptr(scl), _ptr(offs), int(pmode), _ptr(out)))
+        return out
+
     def synth(self, model, phase, sigma, seed, sub0=0, out=None):
         """Synthetic portraits [nsub, nchan, nbin] on device (pplib.py:3342-3377 math)."""
         dev = self.device

@@ -36,6 +36,65 @@ def _dist_info():
     return 0, 1
 
 
+def _gather_objects(obj, rank, world, to_all=False, dst=0):
+    """Every rank's obj, in rank order, on dst (None elsewhere) or on every
+    rank (to_all) -- dist.gather_object / all_gather_object without their
+    per-object pickles of the payload: obj is pickled with protocol 5, so its
+    numpy arrays (a shard's columns: ~3.7 KB per subint at 128 channels)
+    leave the pickle stream as out-of-band buffers; each rank's message is
+    one flat byte tensor [stream | buffer 0 | buffer 1 | ...] (64-byte
+    aligned pieces) moved by tensor collectives -- CPU tensors under gloo,
+    device tensors under nccl (RCCL over xGMI) -- and rebuilt on the
+    receiving rank with the arrays as views of the received bytes."""
+    import pickle
+    import torch
+    import torch.distributed as dist
+    bufs = []
+    head = pickle.dumps(obj, protocol=5, buffer_callback=bufs.append)
+    views = [b.raw() for b in bufs]
+    sizes = [len(head)] + [v.nbytes for v in views]
+    offs = np.zeros(len(sizes) + 1, dtype=np.int64)
+    offs[1:] = np.cumsum([(n + 63) // 64 * 64 for n in sizes])
+    flat = np.empty(int(offs[-1]), dtype=np.uint8)
+    flat[:len(head)] = np.frombuffer(head, dtype=np.uint8)
+    for v, o in zip(views, offs[1:-1]):
+        flat[o:o + v.nbytes] = np.frombuffer(v, dtype=np.uint8)
+    del head, bufs, views
+    dev = torch.device("cuda", torch.cuda.current_device()) \
+        if dist.get_backend() == "nccl" else torch.device("cpu")
+    meta = torch.tensor([len(flat), len(sizes)], dtype=torch.int64, device=dev)
+    metas = [torch.empty_like(meta) for _ in range(world)]
+    dist.all_gather(metas, meta)
+    metas = torch.stack(metas).cpu().numpy()
+    ltot, lcnt = int(metas[:, 0].max()), int(metas[:, 1].max())
+    sz = torch.zeros(lcnt, dtype=torch.int64, device=dev)
+    sz[:len(sizes)] = torch.as_tensor(sizes, dtype=torch.int64)
+    szs = [torch.empty_like(sz) for _ in range(world)]
+    dist.all_gather(szs, sz)
+    msg = torch.zeros(ltot, dtype=torch.uint8, device=dev)
+    msg[:len(flat)] = torch.from_numpy(flat).to(dev)
+    del flat
+    if to_all:
+        got = [torch.empty_like(msg) for _ in range(world)]
+        dist.all_gather(got, msg)
+    else:
+        got = [torch.empty_like(msg) for _ in range(world)] if rank == dst else None
+        dist.gather(msg, got, dst=dst)
+        if rank != dst:
+            return None
+    out = []
+    for r in range(world):
+        a = got[r].cpu().numpy()
+        n = int(metas[r, 1])
+        s = szs[r][:n].cpu().numpy()
+        o = np.zeros(n + 1, dtype=np.int64)
+        o[1:] = np.cumsum((s + 63) // 64 * 64)
+        out.append(pickle.loads(a[:s[0]].tobytes(),
+                                buffers=[a[o[i]:o[i] + s[i]] for i in range(1, n)]))
+        got[r] = None
+    return out
+
+
 def _gc_paused(fn):
     """Run fn with Python's cyclic collector paused: get_TOAs makes few
     containers, but a full collection of the caller's heap (a torch process
@@ -376,16 +435,11 @@ class GetTOAs:
         # every rank ("all")
         t = clock()
         if world > 1:
-            import torch.distributed as dist
-            if self.gather_to == "all":
-                got = [None] * world
-                dist.all_gather_object(got, (shards, durations))
-            else:
-                got = [None] * world if rank == 0 else None
-                dist.gather_object((shards, durations), got, dst=0)
-                if rank != 0:  # the results live on rank 0
-                    del self.ok_idatafiles[n_ok0:]
-                    return
+            got = _gather_objects((shards, durations), rank, world,
+                                  to_all=self.gather_to == "all")
+            if got is None:  # gather_to "root": the results live on rank 0
+                del self.ok_idatafiles[n_ok0:]
+                return
             shards, spans = {}, {}
             for s_r, d_r in got:
                 for ij, v in s_r.items():
