@@ -84,6 +84,16 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 // phi_c} per step pair.  A multiple of every tile's U, so the 16- and
 // 8-channel tiles re-seed at the same harmonics (bitwise the same moments).
 constexpr int kMomReseedSteps = 8;
+// steps in flight of k_fit_taylor's fused first moment pass when it forms X
+// from the data-spectrum cache (two load streams, D and M, per step)
+#ifndef PPF_DSP_U
+#define PPF_DSP_U 2
+#endif
+// ... and when it reads X (one load stream)
+#ifndef PPF_MOM_U
+#define PPF_MOM_U 4
+#endif
+
 
 // X rows: plain loads (the non-temporal hint measured slower here)
 __device__ __forceinline__ double2 xload(const double2* p) { return *p; }
@@ -417,7 +427,7 @@ __global__ __launch_bounds__(kBlock, 3) void k_fit_taylor(FitArgs a) {
       const bool ok = n < a.nchan && (!a.mask || a.mask[(size_t)s * a.nchan + n]);
       const double phic =
           ok ? phase_frac(st0.xc[0], a.freqs[(size_t)s * a.nchan + n], st0.refs, a.P[s]) : 0.0;
-      moment_tile16<DSP ? 2 : 4, DSP>(a, c, 0, n, ok, phic);
+      moment_tile16<DSP ? PPF_DSP_U : PPF_MOM_U, DSP>(a, c, 0, n, ok, phic);
     }
     // T slot 0 is read back below by other waves of this workgroup
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
