@@ -1309,8 +1309,9 @@ int ppf_unpack_subints(ppf_ctx* ctx, int32_t nsub, int32_t npol, int32_t nchan, 
     return fail(ctx, PPF_ERR_INVALID, "pmode %d with npol %d", pmode, npol);
   HIPCHK(ctx, hipSetDevice(ctx->device));
   const int npo = pmode ? 1 : npol;
-  const size_t total = (size_t)nsub * npo * nchan * nbin;
-  const dim3 g((unsigned)((total + 255) / 256));
+  const size_t rows = (size_t)nsub * npo * nchan;
+  if (rows > 0x7fffffffULL) return fail(ctx, PPF_ERR_INVALID, "%zu profiles in one call", rows);
+  const dim3 g((unsigned)rows);
   return timed(ctx, PPF_K_UNPACK, [&] {
     switch (raw_type) {
       case 1:

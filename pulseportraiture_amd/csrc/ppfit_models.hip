@@ -298,27 +298,32 @@ __global__ void k_tscrunch(const double* __restrict__ d, const double* __restric
 // One thread per output sample (raw read once, coalesced along the bins).
 // ---------------------------------------------------------------------------
 template <typename T>
-__global__ void k_unpack(const T* __restrict__ raw, const double* __restrict__ scl,
-                         const double* __restrict__ offs, int nsub, int npol, int nchan,
-                         int nbin, int pmode, double* __restrict__ out) {
+__global__ __launch_bounds__(256) void k_unpack(const T* __restrict__ raw,
+                                                const double* __restrict__ scl,
+                                                const double* __restrict__ offs, int nsub,
+                                                int npol, int nchan, int nbin, int pmode,
+                                                double* __restrict__ out) {
+  // one block per output profile (subint s, polarisation q, channel n): its
+  // scale / offset once, then the row's samples coalesced
   const int npo = pmode ? 1 : npol;
-  const size_t total = (size_t)nsub * npo * nchan * nbin;
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total) return;
-  const int j = (int)(i % nbin);
-  size_t r = i / nbin;
-  const int n = (int)(r % nchan);
-  r /= nchan;
+  const size_t row = blockIdx.x;
+  const int n = (int)(row % nchan);
+  const size_t r = row / nchan;
   const int q = (int)(r % npo);
   const size_t s = r / npo;
-  auto val = [&](int p) {
-    const size_t m = (s * npol + p) * nchan + n;
-    return fma((double)raw[m * nbin + j], scl[m], offs[m]);
-  };
-  double v;
-  if (pmode == 1) v = val(0) + val(1);
-  else v = val(pmode == 2 ? 0 : q);
-  out[i] = v;
+  const size_t m0 = (s * npol + (pmode ? 0 : q)) * nchan + n;
+  const size_t m1 = (s * npol + 1) * nchan + n;  // pmode 1 only (npol >= 2)
+  const double sc0 = scl[m0], of0 = offs[m0];
+  const double sc1 = pmode == 1 ? scl[m1] : 0.0, of1 = pmode == 1 ? offs[m1] : 0.0;
+  const T* __restrict__ r0 = raw + m0 * nbin;
+  const T* __restrict__ r1 = raw + (pmode == 1 ? m1 : m0) * nbin;
+  double* __restrict__ o = out + row * nbin;
+  for (int j = threadIdx.x; j < nbin; j += blockDim.x) {
+    double v = fma((double)r0[j], sc0, of0);
+    if (pmode == 1) v = v + fma((double)r1[j], sc1, of1);
+    o[j] = v;
+  }
+  (void)nsub;
 }
 
 // ---------------------------------------------------------------------------

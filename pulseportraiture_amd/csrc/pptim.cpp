@@ -19,6 +19,10 @@
 #include <new>
 #include <string>
 #include <thread>
+
+#ifndef PPT_MIN_ROWS_PER_THREAD
+#define PPT_MIN_ROWS_PER_THREAD 2048
+#endif
 #include <vector>
 
 // Source hash of this build (pulseportraiture_amd/build.py compares it with
@@ -295,7 +299,9 @@ extern "C" int ppt_format_rows(int64_t n, int32_t nfield, const ppt_field* field
   }
   unsigned hw = std::thread::hardware_concurrency();
   int64_t nt = nthreads > 0 ? nthreads : static_cast<int64_t>(hw ? (hw < 8 ? hw : 8) : 1);
-  const int64_t min_rows = 16384;  // below this a thread costs more than it saves (measured)
+  // rows per thread at least: below this a thread's start costs more than it
+  // saves (r06, on the GPU box: 7,000 / 3,000-row pieces of a get_TOAs call)
+  const int64_t min_rows = PPT_MIN_ROWS_PER_THREAD;
   if (nt > (n + min_rows - 1) / min_rows) nt = (n + min_rows - 1) / min_rows;
   if (nt < 1) nt = 1;
   auto* t = new (std::nothrow) ppt_text;

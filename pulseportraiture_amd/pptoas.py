@@ -95,6 +95,35 @@ def _gather_objects(obj, rank, world, to_all=False, dst=0):
     return out
 
 
+_POOL = None
+
+
+def _par_concat(parts):
+    """{key: np.concatenate(pieces)} with the pieces copied into place on a
+    few host threads (np.copyto releases the GIL); the same arrays as
+    np.concatenate's."""
+    global _POOL
+    from .toas import _host_threads
+    nt = min(4, _host_threads())
+    if nt < 2:
+        return {k: np.concatenate(v) for k, v in parts.items()}
+    if _POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+        _POOL = ThreadPoolExecutor(max_workers=nt, thread_name_prefix="pptoas-cat")
+    out, jobs = {}, []
+    for k, v in parts.items():
+        a = np.empty((sum(len(x) for x in v),) + v[0].shape[1:],
+                     dtype=np.result_type(*[x.dtype for x in v]))
+        o = 0
+        for x in v:
+            jobs.append(_POOL.submit(np.copyto, a[o:o + len(x)], x))
+            o += len(x)
+        out[k] = a
+    for j in jobs:
+        j.result()
+    return out
+
+
 def _gc_paused(fn):
     """Run fn with Python's cyclic collector paused: get_TOAs makes few
     containers, but a full collection of the caller's heap (a torch process
@@ -1228,8 +1257,14 @@ class GetTOAs:
             def cat(k):
                 return shards[0][k]
         else:
+            # the per-channel columns (most of the bytes) joined on host
+            # threads: a fresh [nsub, nchan] array's first-touch page faults
+            # and copies are most of _finish's time
+            big = _par_concat({k: [sh[k] for sh in shards]
+                               for k in ("scales", "scale_errs", "chsnrs")})
+
             def cat(k):
-                return np.concatenate([sh[k] for sh in shards])
+                return big[k] if k in big else np.concatenate([sh[k] for sh in shards])
         dense = nok == nsub  # ok_isubs is then every subint, in order
 
         def spread(v, tail=(), dtype=np.float64):

@@ -52,3 +52,13 @@ pr.disable()
 st = pstats.Stats(pr)
 st.sort_stats("cumulative").print_stats(40)
 st.sort_stats("tottime").print_stats(30)
+st.print_callers("as_tensor")
+st.print_callers("copy_")
+# the same calls with the device drained before each one
+rows = []
+for _ in range(8):
+    torch.cuda.synchronize()
+    gt, a, b = run()
+    rows.append(dict(gt.phase_s, call=a, write=b))
+print("drained first, median ms over 8 calls:",
+      {k: round(float(np.median([r.get(k, 0.0) for r in rows])) * 1e3, 3) for k in keys})
