@@ -40,7 +40,7 @@ def timed(name, fn):
 E.Engine.fit_batch = timed("engine.fit_batch (launch)", E.Engine.fit_batch)
 E.FitPipeline.submit = timed("pipeline submit", E.FitPipeline.submit)
 E.FitPipeline.collect = timed("pipeline collect (wait)", E.FitPipeline.collect)
-for fr in [None, (1.0,), (0.8, 0.2), (0.6, 0.25, 0.15), (0.3, 0.25, 0.2, 0.15, 0.1), (0.7, 0.3)]:
+for fr in [None, (1.0,), (0.8, 0.2), (0.75, 0.25), (0.65, 0.35), (0.6, 0.3, 0.1), (0.55, 0.3, 0.15), (0.7, 0.3)]:
   if fr is not None:
     pptoas.GetTOAs.pipeline_fracs = fr
   print("pipeline_fracs", pptoas.GetTOAs.pipeline_fracs)
