@@ -70,8 +70,8 @@ FP64_PEAK_TFLOPS = 78.6  # AMD MI355X spec, fp64 vector = fp64 matrix (not in th
 # HBM bytes per launch per kernel from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
 # passes over this same bench (tools/profile_r03.sh + tools/pmc_summary.py)
 PMC_TRAFFIC = {c: os.path.join(ROOT, "profiles", "%s_pmc_traffic_%s.json" % (r, c))
-               for c, r in (("headline", "r05"), ("scattering", "r05"), ("gm", "r05"),
-                            ("ppalign", "r05"))}
+               for c, r in (("headline", "r06"), ("scattering", "r06"), ("gm", "r06"),
+                            ("ppalign", "r06"))}
 KERNEL_SYMBOL = {"solve": "k_scat_sweep", "data_xspec": "k_data_xspec<10>",
                  "rot_accum": "k_rot_accum_w",
                  "post": "k_post<false>", "guess": "k_guess_w", "moments": "k_moments<4, false>",

@@ -98,25 +98,41 @@ def _gather_objects(obj, rank, world, to_all=False, dst=0):
 _POOL = None
 
 
-def _par_concat(parts):
-    """{key: np.concatenate(pieces)} with the pieces copied into place on a
-    few host threads (np.copyto releases the GIL); the same arrays as
-    np.concatenate's."""
+def _pool():
+    """The host-thread pool of _par_concat / _par_map (None: one thread)."""
     global _POOL
     from .toas import _host_threads
     nt = min(4, _host_threads())
     if nt < 2:
-        return {k: np.concatenate(v) for k, v in parts.items()}
+        return None
     if _POOL is None:
         from concurrent.futures import ThreadPoolExecutor
-        _POOL = ThreadPoolExecutor(max_workers=nt, thread_name_prefix="pptoas-cat")
+        _POOL = ThreadPoolExecutor(max_workers=nt, thread_name_prefix="pptoas")
+    return _POOL
+
+
+def _par_map(fn, items):
+    """[fn(x) for x in items], the calls on host threads."""
+    pool = _pool()
+    if pool is None:
+        return [fn(x) for x in items]
+    return [f.result() for f in [pool.submit(fn, x) for x in items]]
+
+
+def _par_concat(parts):
+    """{key: np.concatenate(pieces)} with the pieces copied into place on a
+    few host threads (np.copyto releases the GIL); the same arrays as
+    np.concatenate's."""
+    pool = _pool()
+    if pool is None:
+        return {k: np.concatenate(v) for k, v in parts.items()}
     out, jobs = {}, []
     for k, v in parts.items():
         a = np.empty((sum(len(x) for x in v),) + v[0].shape[1:],
                      dtype=np.result_type(*[x.dtype for x in v]))
         o = 0
         for x in v:
-            jobs.append(_POOL.submit(np.copyto, a[o:o + len(x)], x))
+            jobs.append(pool.submit(np.copyto, a[o:o + len(x)], x))
             o += len(x)
         out[k] = a
     for j in jobs:
@@ -866,8 +882,14 @@ class GetTOAs:
 
         def okrows(a):
             return a if dense else a[ok_isubs]
-        uniform = {k: bool(len(ok_isubs)) and bool((okrows(a) == okrows(a)[0]).all())
-                   for k, a in (("freqs", data.freqs), ("mask", mask), ("weights", data.weights))}
+
+        def rows_equal(a):
+            a = okrows(a)
+            return bool(len(ok_isubs)) and bool((a == a[0]).all())
+        # freqs and weights compared on two host threads (numpy releases the
+        # GIL); equal weight rows make the mask rows equal too
+        ru = _par_map(rows_equal, [data.freqs, data.weights])
+        uniform = {"freqs": ru[0], "weights": ru[1], "mask": ru[1] or rows_equal(mask)}
         mm = self._models(data, fit_scat, quiet, uniform["freqs"])
         if mm is None:
             if not quiet:
@@ -876,7 +898,7 @@ class GetTOAs:
         models, midx, _ = mm
         if self._irf_active():
             models, midx = self._irf_models(models, midx, data, ok_isubs)
-        nchx = wn.sum(axis=1)
+        nchx = np.count_nonzero(wn, axis=1)
         allok = nchx == nchan
         # the tobs flag's values: typed when the durations are numbers
         tobs = np.asarray(data.subtimes)
