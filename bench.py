@@ -8,7 +8,10 @@ Nelder-Mead), Taylor moments of the cross-spectrum (k_moments) and the
 trust-ncg fit on them (k_fit_taylor) -- or, for scattering fits, the split
 exact sweeps (k_scat_sweep / k_scat_step) -- and the post-fit (k_post:
 zero-covariance frequency, phi at nu_out, Woodbury covariance, snr, chi2),
-then the per-TOA results copied to the host.  Data: synthetic portraits from
+then the per-TOA results copied to the host.  Steps run back to back the way
+a production loop does: step k + 1 is queued before step k's results are
+read (their D2H on a side stream behind step k's kernels), so a step's host
+side overlaps the next step's fits.  Data: synthetic portraits from
 example.gmodel with injected phi/DM and sigma=1.5 Philox noise, generated on
 the device before timing.
 
@@ -459,15 +462,21 @@ def main():
     w, data, kw, tau_g = synth_inputs(eng, fit_config, nsub, args.seed, rank * nsub)
     torch.cuda.synchronize()
     small = ["params", "param_errs", "nu_out", "red_chi2", "snr", "status", "nfev"]
-    from pulseportraiture_amd.engine import results_to_host
+    from pulseportraiture_amd.engine import results_to_host_async
+    side = torch.cuda.Stream(eng.device)
 
-    def step():
+    def submit():
         out = eng.fit_batch(data, kw["model"], kw["freqs"], kw["P"], kw["init"], flags,
                             nu_fit=kw["nu"], log10_tau=log10_tau, guess=True, guess_Ns=100,
                             guess_tau=kw["gtau"])
-        # the per-TOA results on the host: one D2H of the packed span that
-        # holds them (plus nfev / status), waited for
-        return out, results_to_host(out, small, eng.stream)
+        # the per-TOA results on their way to the host: one D2H of the packed
+        # span that holds them (plus nfev / status) on a side stream, behind
+        # this call's kernels only
+        return out, results_to_host_async(out, small, eng.stream, side)
+
+    def step():
+        out, pend = submit()
+        return out, pend.wait()
 
     if config == "get_toas":
         return main_get_toas(args, eng, rank, world, w, data, step, desc)
@@ -482,8 +491,16 @@ def main():
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    # steps back to back: step k + 1 is queued before step k's results are
+    # read, so the host side of a step (fit_batch's set-up, the wait for the
+    # results) runs while the device fits the next batch
+    prev = None
     for _ in range(args.steps):
-        out, host = step()
+        cur = submit()
+        if prev is not None:
+            prev[1].wait()
+        prev = cur
+    out, host = prev[0], prev[1].wait()
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()

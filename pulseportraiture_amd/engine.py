@@ -221,6 +221,14 @@ def results_to_host(out, keys=None, stream=None):
     return res
 
 
+def results_to_host_async(out, keys, stream, side):
+    """results_to_host deferred: marks the end of the fit call on `stream`
+    now and returns a handle whose wait() copies the results on the `side`
+    stream (behind that mark only) and returns them -- so the next call can
+    be queued before this one's results are read."""
+    return _PendingHost(out, keys, stream, side)
+
+
 class Engine:
     """One libppfit context on one HIP device (one per process/GPU)."""
 
