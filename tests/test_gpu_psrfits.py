@@ -132,3 +132,30 @@ def test_tscrunch_psrfits_and_get_toas(gpu, tmp_path):
     finally:
         os.chdir(cwd)
     assert len(lines[0]) == 1 and lines[0] == lines[1]
+
+
+@pytest.mark.parametrize("dtype", ["uint8", "int16", "float32"])
+@pytest.mark.parametrize("pmode", [0, 1, 2])
+def test_unpack_subints_raw_types(gpu, dtype, pmode):
+    """Engine.unpack_subints (ppf_unpack_subints, one block per output
+    profile) for every PSRFITS sample type and pscrunch mode: DATA * DAT_SCL
+    + DAT_OFFS (one fma, so within an ulp of numpy's two roundings), AA + BB
+    (pmode 1), the first polarisation (pmode 2), every polarisation (0);
+    ragged shapes (nbin not a multiple of the block, odd nchan)."""
+    import torch
+    rng = np.random.default_rng(5)
+    nsub, npol, nchan, nbin = 3, 2, 7, 300
+    if dtype == "float32":
+        raw = rng.normal(size=(nsub, npol, nchan, nbin)).astype(np.float32)
+    else:
+        info = np.iinfo(dtype)
+        raw = rng.integers(info.min, info.max, size=(nsub, npol, nchan, nbin)).astype(dtype)
+    scl = rng.uniform(1e-3, 2.0, size=(nsub, npol, nchan))
+    offs = rng.normal(size=(nsub, npol, nchan))
+    dev = gpu.device
+    out = gpu.unpack_subints(torch.as_tensor(raw, device=dev), torch.as_tensor(scl, device=dev),
+                             torch.as_tensor(offs, device=dev), pmode).cpu().numpy()
+    phys = raw.astype(np.float64) * scl[..., None] + offs[..., None]
+    want = phys if pmode == 0 else (phys[:, :1] + phys[:, 1:2] if pmode == 1 else phys[:, :1])
+    assert out.shape == want.shape
+    np.testing.assert_allclose(out, want, rtol=0, atol=4e-16 * np.abs(want).max())
