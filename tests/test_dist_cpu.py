@@ -101,3 +101,60 @@ def test_rank_slices_equal_single_process_subints():
     np.testing.assert_array_equal(r1.phase, whole.phase[nsub:])
     np.testing.assert_array_equal(synth.workload_data_host(r1),
                                   synth.workload_data_host(whole)[nsub:])
+
+
+def _gather_payload(rank):
+    """Arrays of every layout the protocol-5 gather must carry: C and F order,
+    strided views (pickled in-band), empty, odd byte counts, object arrays."""
+    rng = np.random.default_rng(50 + rank)
+    base = rng.standard_normal((5 + rank, 7))
+    return {
+        "rank": rank,
+        "c": base,
+        "f": np.asfortranarray(rng.standard_normal((3, 4 + rank))),
+        "strided": base[::2, 1::3],
+        "empty": np.zeros((0, 3), dtype=np.float32),
+        "odd": rng.integers(0, 255, 13 + 2 * rank, dtype=np.uint8),
+        "i16": rng.integers(-9, 9, (2, 3), dtype=np.int16),
+        "obj": np.array(["a" * (rank + 1), None, 3], dtype=object),
+        "tail": [np.float64(rank), "x" * 100 * (rank + 1)],
+    }
+
+
+def _gather_equal(a, b):
+    assert a.keys() == b.keys()
+    for k in a:
+        if isinstance(a[k], np.ndarray):
+            assert a[k].dtype == b[k].dtype and a[k].shape == b[k].shape, k
+            assert a[k].tolist() == b[k].tolist(), k
+        else:
+            assert a[k] == b[k], k
+
+
+def _gather_worker(rank, world, port, out_dir):
+    from pulseportraiture_amd import pptoas
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        obj = _gather_payload(rank)
+        root = pptoas._gather_objects(obj, rank, world)
+        every = pptoas._gather_objects(obj, rank, world, to_all=True)
+        dst1 = pptoas._gather_objects(obj, rank, world, dst=1)
+        assert (root is None) == (rank != 0)
+        assert (dst1 is None) == (rank != 1)
+        for got in [g for g in (root, dst1) if g is not None] + [every]:
+            assert len(got) == world
+            for r in range(world):
+                _gather_equal(got[r], _gather_payload(r))
+        open(os.path.join(out_dir, "ok%d" % rank), "w").close()
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_gloo_ws2_gather_objects_roundtrip():
+    """get_TOAs' shard gather (pptoas._gather_objects) returns every rank's
+    object unchanged, in rank order, to the root, to another rank and to all."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_gather_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        assert sorted(os.listdir(d)) == ["ok0", "ok1"]
