@@ -48,10 +48,16 @@
  *    with a message, never a silent fallback): nbin must be a power of two
  *    in [64, 8192] (the register / LDS FFTs and the Taylor power tables are
  *    built per power of two; the reference's numpy rfft takes any length,
- *    pptoaslib.py:976-978), and nchan <= PPF_MAX_NCHAN (the per-channel
- *    metadata of a subint is staged in LDS; the reference takes any channel
- *    count).  A caller with other shapes must resample (nbin) or split the
- *    channels itself; there is no generic-length path.
+ *    pptoaslib.py:976-978), and nchan <= PPF_MAX_NCHAN (the reference
+ *    takes any channel count; 16384 covers every receiver in use).  A caller
+ *    with another nbin must resample; there is no generic-length path.
+ *  - Channel counts: up to PPF_LDS_NCHAN a fit workgroup keeps its subint's
+ *    per-channel tables (frequencies, weights, dispersion derivatives, the
+ *    fitted-channel list) in LDS; above it (or under PPF_OPT_HBM_TABLES) the
+ *    same kernels, instantiated for it, keep them in an HBM workspace slice
+ *    per workgroup, and scattering fits take one workgroup per subint
+ *    (PPF_OPT_SCAT_SPLIT is not used).  The fits are bitwise the same either
+ *    way (tests/test_gpu_wide.py); only their speed differs.
  */
 #ifndef PPFIT_H
 #define PPFIT_H
@@ -68,7 +74,8 @@ extern "C" {
 #define PPF_ERR_UNSUPPORTED -3
 #define PPF_ERR_NOMEM -4
 
-#define PPF_MAX_NCHAN 2048
+#define PPF_MAX_NCHAN 16384
+#define PPF_LDS_NCHAN 2048
 #define PPF_VERSION 1
 
 /* kernel ids for ppf_get_kernel_time */
@@ -119,13 +126,16 @@ int ppf_set_pipeline(ppf_ctx* ctx, int32_t pieces);
  *   PPF_OPT_FUSE_MOMENTS 1: the first Taylor moment pass runs inside
  *                        k_fit_taylor (default); 0: its own k_moments launch.
  *   PPF_OPT_GUESS_WAVE   1: the single-wave guess kernel takes the subints it
- *                        covers (default); 0: every guess in k_guess.       */
+ *                        covers (default); 0: every guess in k_guess.
+ *   PPF_OPT_HBM_TABLES   1: the per-channel tables in HBM at every channel
+ *                        count (default 0: only above PPF_LDS_NCHAN).       */
 #define PPF_OPT_SCAT_GRAPH 0
 #define PPF_OPT_SCAT_SPLIT 1
 #define PPF_OPT_SCAT_TAIL 2
 #define PPF_OPT_FUSE_MOMENTS 3
 #define PPF_OPT_GUESS_WAVE 4
-#define PPF_NUM_OPTS 5
+#define PPF_OPT_HBM_TABLES 5
+#define PPF_NUM_OPTS 6
 int ppf_set_option(ppf_ctx* ctx, int32_t option, int32_t value);
 int ppf_get_option(const ppf_ctx* ctx, int32_t option, int32_t* value);
 /* Upper bound on workspace bytes the context may hold (default 32 GiB). */

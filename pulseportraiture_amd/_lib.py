@@ -28,7 +28,8 @@ PPF_SPEC_STORE = 1
 PPF_SPEC_USE = 2
 PPF_SELFTEST_N = 10
 # ppf_set_option ids (include/ppfit.h)
-OPTIONS = {"scat_graph": 0, "scat_split": 1, "scat_tail": 2, "fuse_moments": 3, "guess_wave": 4}
+OPTIONS = {"scat_graph": 0, "scat_split": 1, "scat_tail": 2, "fuse_moments": 3, "guess_wave": 4,
+           "hbm_tables": 5}
 PPF_PHASE_N = 32
 
 _dp = ctypes.c_void_p  # device pointers travel as plain addresses

@@ -64,7 +64,7 @@ struct ppf_ctx {
   double* trace = nullptr;  // solver trace buffer (ppf_set_trace), device
   int trace_cap = 0;
   // launch-schedule options (ppf_set_option; include/ppfit.h)
-  int opt[PPF_NUM_OPTS] = {1, 1, 512, 1, 1};
+  int opt[PPF_NUM_OPTS] = {1, 1, 512, 1, 1, 0};
   double ktime[PPF_NUM_KERNELS] = {0};
   int64_t klaunch[PPF_NUM_KERNELS] = {0};
 };
@@ -247,6 +247,13 @@ int resolve_timing(ppf_ctx* ctx) {
     default: break;                                   \
   }
 
+// WD: the instantiation with the per-channel tables in HBM (chan_tables)
+#define WIDE_SWITCH(W, ...)                                \
+  do {                                                     \
+    if (W) { constexpr bool WD = true; __VA_ARGS__; }      \
+    else { constexpr bool WD = false; __VA_ARGS__; }       \
+  } while (0)
+
 // Template spectra for nrow rows of nbin (DC zeroed when zero_dc).
 int model_spectra(ppf_ctx* ctx, int nrow, int nbin, const double* model, int zero_dc, Buffer& buf,
                   double2** M, double** pn, double** M2 = nullptr) {
@@ -278,13 +285,15 @@ size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 // launch; the moment passes form X from the data-spectrum cache when fa.Dsp is set
 void launch_fit_taylor(const ppf_ctx* ctx, dim3 g, size_t lds, hipStream_t st, const FitArgs& fa) {
   const bool mom = ctx->opt[PPF_OPT_FUSE_MOMENTS] != 0;
-  if (fa.Dsp) {
-    if (mom) hipLaunchKernelGGL((k_fit_taylor<true, true>), g, dim3(kBlock), lds, st, fa);
-    else hipLaunchKernelGGL((k_fit_taylor<false, true>), g, dim3(kBlock), lds, st, fa);
-  } else {
-    if (mom) hipLaunchKernelGGL((k_fit_taylor<true, false>), g, dim3(kBlock), lds, st, fa);
-    else hipLaunchKernelGGL((k_fit_taylor<false, false>), g, dim3(kBlock), lds, st, fa);
-  }
+  WIDE_SWITCH(fa.gdyn != nullptr, {
+    if (fa.Dsp) {
+      if (mom) hipLaunchKernelGGL((k_fit_taylor<true, true, WD>), g, dim3(kBlock), lds, st, fa);
+      else hipLaunchKernelGGL((k_fit_taylor<false, true, WD>), g, dim3(kBlock), lds, st, fa);
+    } else {
+      if (mom) hipLaunchKernelGGL((k_fit_taylor<true, false, WD>), g, dim3(kBlock), lds, st, fa);
+      else hipLaunchKernelGGL((k_fit_taylor<false, false, WD>), g, dim3(kBlock), lds, st, fa);
+    }
+  });
 }
 
 void launch_moments(dim3 g, hipStream_t st, const FitArgs& fa) {
@@ -480,7 +489,13 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   const size_t bC = (size_t)nchan * sizeof(double);
   const size_t bAcc = (size_t)2 * nchan * 10 * sizeof(double);
   const size_t bW = (size_t)nchan * 8 * sizeof(double);
-  const size_t per_sub = bX + bT + 2 * bR + 2 * bC + sizeof(SolveState) + bAcc + bW;
+  // per-channel tables in HBM (the WIDE kernels, ppfit_kernels.hpp chan_tables)
+  const bool wide = nchan > PPF_LDS_NCHAN || ctx->opt[PPF_OPT_HBM_TABLES] != 0;
+  const size_t bG = wide ? align256(std::max(align256((size_t)nchan * (5 * sizeof(double) +
+                                                                        sizeof(int))),
+                                             xspec_dyn_lds(nchan)))
+                         : 0;
+  const size_t per_sub = bX + bT + 2 * bR + 2 * bC + sizeof(SolveState) + bAcc + bW + bG;
   int64_t chunk = ctx->ws_limit / (int64_t)(per_sub + 1024);
   if (chunk < 1) chunk = 1;
   if (chunk > d->nsub) chunk = d->nsub;
@@ -494,7 +509,8 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   const size_t offAcc = align256(offSt + cs * sizeof(SolveState));
   const size_t offW = align256(offAcc + cs * bAcc);
   const size_t offT = align256(offW + cs * bW);
-  const size_t total = align256(offT + cs * bT);
+  const size_t offG = align256(offT + cs * bT);
+  const size_t total = align256(offG + cs * bG);
   if (int r = ensure(ctx, ctx->ws, total)) return r;
   char* base = static_cast<char*>(ctx->ws.p);
 
@@ -523,6 +539,8 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   sa.sig = reinterpret_cast<double*>(base + offSig);
   sa.dsum = reinterpret_cast<double*>(base + offDs);
   sa.tw = tw;
+  sa.gdyn = wide ? reinterpret_cast<unsigned char*>(base + offG) : nullptr;
+  sa.gdyn_stride = bG;
 
   FitArgs fa{};
   fa.nchan = nchan;
@@ -562,6 +580,8 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   fa.st = reinterpret_cast<SolveState*>(base + offSt);
   fa.acc = reinterpret_cast<double*>(base + offAcc);
   fa.wsc = reinterpret_cast<double*>(base + offW);
+  fa.gdyn = sa.gdyn;
+  fa.gdyn_stride = bG;
   fa.T = taylor ? reinterpret_cast<double*>(base + offT) : nullptr;
   fa.tw = tw;
   fa.vpow = nullptr;
@@ -589,17 +609,20 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
   fa.o_grad = o->grad;
   fa.o_hess = o->hess;
 
-  const size_t lds_meta = align256((size_t)nchan * (5 * sizeof(double) + sizeof(int)));
+  // dynamic LDS of the Meta kernels (none for the WIDE ones)
+  const size_t lds_meta =
+      wide ? 0 : align256((size_t)nchan * (5 * sizeof(double) + sizeof(int)));
+  const size_t lds_xspec = wide ? 0 : xspec_dyn_lds(nchan);
   // k_fit_taylor keeps moments [0, tnl) of T slot 0 in LDS (all of them when
-  // they fit beside kTaylorBlocksPerCU - 1 other blocks)
-  fa.tnl = taylor ? taylor_lds_moments(nchan, lds_meta) : 0;
+  // they fit beside kTaylorBlocksPerCU - 1 other blocks; none when WIDE)
+  fa.tnl = taylor && !wide ? taylor_lds_moments(nchan, lds_meta) : 0;
   fa.tlds = fa.tnl > 0 ? (int)lds_meta : 0;
   const size_t lds_taylor = lds_meta + (size_t)nchan * fa.tnl * sizeof(double);
   // trust-ncg scattering fits: every evaluation split over blocks of >= 64
   // fitted channels (k_scat_sweep / k_scat_step)
   // (PPF_OPT_SCAT_SPLIT = 0: one block per subint, k_solve<true>)
   const bool split_scat = ctx->opt[PPF_OPT_SCAT_SPLIT] && d->fit_flags[3] &&
-                          d->method == PPF_METHOD_TRUST_NCG;
+                          d->method == PPF_METHOD_TRUST_NCG && !wide;
   const int split = std::max(1, std::min(16, nchan / 64));
   // the two-phase sweep's rows (any block's channel range at split or more)
   const size_t lds_scat = PPF_SCAT_TWO_PHASE ? scat_sweep_lds(nchan, split) : lds_meta;
@@ -663,12 +686,16 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
         fp.T = fa.T + (size_t)off * 2 * nchan * kMT;
         fp.acc = fa.acc + (size_t)off * 2 * nchan * 10;
         fp.wsc = fa.wsc + (size_t)off * nchan * 8;
+        if (wide) {
+          sp.gdyn = sa.gdyn + (size_t)off * bG;
+          fp.gdyn = sp.gdyn;
+        }
         bind_spec(sp, fp, s0 + off);
         if (prev_x) HIPCHK(ctx, hipStreamWaitEvent(st, prev_x, 0));
         if (int r = timed_on(ctx, PPF_K_DATA_XSPEC, st, [&] {
-              LOGN_SWITCH(logN, hipLaunchKernelGGL(k_data_xspec<LG>, dim3(n),
+              LOGN_SWITCH(logN, WIDE_SWITCH(wide, hipLaunchKernelGGL((k_data_xspec<LG, WD>), dim3(n),
                                                    dim3(XspecCfg<LG>::WPB * 64),
-                                                   xspec_dyn_lds(nchan), st, sp));
+                                                   lds_xspec, st, sp)));
             }))
           return r;
         if (int r = sync_event(ctx, ev++, &prev_x)) return r;
@@ -693,12 +720,15 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
         // fitted): the one-workgroup scattering solve and post-fit, as on
         // one queue (both exit at once for every other subint)
         if (int r = timed_on(ctx, PPF_K_SOLVE, st, [&] {
-              hipLaunchKernelGGL(k_solve<true>, dim3(n), dim3(kBlock), lds_meta, st, fp);
+              WIDE_SWITCH(wide, hipLaunchKernelGGL((k_solve<true, WD>), dim3(n), dim3(kBlock),
+                                                   lds_meta, st, fp));
             }))
           return r;
         if (int r = timed_on(ctx, PPF_K_POST, st, [&] {
-              hipLaunchKernelGGL(k_post<false>, dim3(n), dim3(kBlock), lds_meta, st, fp);
-              hipLaunchKernelGGL(k_post<true>, dim3(n), dim3(kBlock), lds_meta, st, fp);
+              WIDE_SWITCH(wide, {
+                hipLaunchKernelGGL((k_post<false, WD>), dim3(n), dim3(kBlock), lds_meta, st, fp);
+                hipLaunchKernelGGL((k_post<true, WD>), dim3(n), dim3(kBlock), lds_meta, st, fp);
+              });
             }))
           return r;
         if (o->errs_out)
@@ -720,8 +750,9 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
     fa.sub0 = (int)s0;
     bind_spec(sa, fa, s0);
     if (int r = timed(ctx, PPF_K_DATA_XSPEC, [&] {
-          LOGN_SWITCH(logN, hipLaunchKernelGGL(k_data_xspec<LG>, dim3(nc), dim3(XspecCfg<LG>::WPB * 64), xspec_dyn_lds(nchan),
-                                               ctx->stream, sa));
+          LOGN_SWITCH(logN, WIDE_SWITCH(wide, hipLaunchKernelGGL((k_data_xspec<LG, WD>), dim3(nc),
+                                                                 dim3(XspecCfg<LG>::WPB * 64),
+                                                                 lds_xspec, ctx->stream, sa)));
         }))
       return r;
     if (int r = timed(ctx, PPF_K_GUESS, [&] {
@@ -734,20 +765,28 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
     // each subint runs in exactly one of the exact phase-only / scattering /
     // fused Taylor variants (the others exit at once)
     if (int r = timed(ctx, PPF_K_SOLVE, [&] {
-          if (tnc) {
-            hipLaunchKernelGGL(k_tnc<false>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
-            hipLaunchKernelGGL(k_tnc<true>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
-            return;
-          }
-          if (ncg) {
-            hipLaunchKernelGGL(k_ncg<false>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
-            hipLaunchKernelGGL(k_ncg<true>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
-            return;
-          }
-          if (exact)
-            hipLaunchKernelGGL(k_solve<false>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
-          if (!split_scat)
-            hipLaunchKernelGGL(k_solve<true>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
+          WIDE_SWITCH(wide, {
+            if (tnc) {
+              hipLaunchKernelGGL((k_tnc<false, WD>), dim3(nc), dim3(kBlock), lds_meta, ctx->stream,
+                                 fa);
+              hipLaunchKernelGGL((k_tnc<true, WD>), dim3(nc), dim3(kBlock), lds_meta, ctx->stream,
+                                 fa);
+              return;
+            }
+            if (ncg) {
+              hipLaunchKernelGGL((k_ncg<false, WD>), dim3(nc), dim3(kBlock), lds_meta, ctx->stream,
+                                 fa);
+              hipLaunchKernelGGL((k_ncg<true, WD>), dim3(nc), dim3(kBlock), lds_meta, ctx->stream,
+                                 fa);
+              return;
+            }
+            if (exact)
+              hipLaunchKernelGGL((k_solve<false, WD>), dim3(nc), dim3(kBlock), lds_meta,
+                                 ctx->stream, fa);
+            if (!split_scat)
+              hipLaunchKernelGGL((k_solve<true, WD>), dim3(nc), dim3(kBlock), lds_meta,
+                                 ctx->stream, fa);
+          });
         }))
       return r;
     if (split_scat && !tnc && !ncg) {
@@ -860,8 +899,12 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
         return r;
     }
     if (int r = timed(ctx, PPF_K_POST, [&] {
-          hipLaunchKernelGGL(k_post<false>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
-          hipLaunchKernelGGL(k_post<true>, dim3(nc), dim3(kBlock), lds_meta, ctx->stream, fa);
+          WIDE_SWITCH(wide, {
+            hipLaunchKernelGGL((k_post<false, WD>), dim3(nc), dim3(kBlock), lds_meta, ctx->stream,
+                               fa);
+            hipLaunchKernelGGL((k_post<true, WD>), dim3(nc), dim3(kBlock), lds_meta, ctx->stream,
+                               fa);
+          });
         }))
       return r;
     if (o->errs_out)  // the sigma each channel was fitted with (k_data_xspec)

@@ -1365,7 +1365,7 @@ struct SolveShared {
   int same;             // the proposal repeats the last evaluated point
 };
 
-template <bool SCAT>
+template <bool SCAT, bool WIDE>
 __global__ __launch_bounds__(kBlock) void k_solve(FitArgs a) {
   extern __shared__ __align__(16) unsigned char dyn[];
   __shared__ SolveShared sh;
@@ -1374,7 +1374,7 @@ __global__ __launch_bounds__(kBlock) void k_solve(FitArgs a) {
   const int lane = tid & 63;
   if (a.method != PPF_METHOD_TRUST_NCG) return;  // k_tnc owns TNC fits
   if ((a.st[c].scat != 0) != SCAT) return;  // the other variant owns this subint
-  const Meta m = load_meta(a, c, s, dyn, &sh.nok);
+  const Meta m = load_meta(a, c, s, chan_tables<WIDE>(a, dyn), &sh.nok);
   SolveState& st = a.st[c];
   const double P = a.P[s];
   if (tid < 5) sh.x[tid] = st.x[tid];
@@ -2199,7 +2199,7 @@ struct PostShared {
 
 // zero-covariance frequencies, outputs at nu_out and the with-scales
 // covariance of one subint (all threads of the block)
-template <bool SCAT>
+template <bool SCAT, bool W>  // W: one copy per k_post instantiation (its only caller)
 __device__ void post_subint(const FitArgs& a, int c, int s, unsigned char* dyn, PostShared& sh) {
   const int tid = threadIdx.x;
   const int nchan = a.nchan;
@@ -2468,7 +2468,7 @@ __device__ void post_subint(const FitArgs& a, int c, int s, unsigned char* dyn, 
 // the compiler meets with 168 VGPRs (three waves per SIMD, no spills).  r04
 // A/B at config 2: four per CU (128 VGPRs, 77 spilled) 0.47 -> 0.56 ms (r02's
 // code had preferred the cap).  The scattering variant keeps its registers.
-template <bool SCAT>
+template <bool SCAT, bool WIDE>
 #ifndef PPF_POST_SCAT_WG_PER_CU
 // two workgroups per CU (256 VGPRs, 12 B/lane spilled) instead of one (256 +
 // 7 AGPRs): config 3's k_post<true> 1.30 -> 1.09-1.10 ms, bitwise the same
@@ -2481,7 +2481,7 @@ __global__ __launch_bounds__(kBlock, SCAT ? PPF_POST_SCAT_WG_PER_CU : PPF_POST_W
   __shared__ PostShared sh;
   const int c = blockIdx.x, s = a.sub0 + c;
   if ((a.st[c].scat_post != 0) != SCAT) return;
-  post_subint<SCAT>(a, c, s, dyn, sh);
+  post_subint<SCAT, WIDE>(a, c, s, chan_tables<WIDE>(a, dyn), sh);
 }
 
 }  // namespace ppf

@@ -28,7 +28,21 @@ struct SpecArgs {
   double* dsum;            // chunk [c][nchan]
   const double2* tw;
   double2* D;              // chunk [c][nchan][NHP] data spectra (spec cache) or null
+  unsigned char* gdyn;     // WIDE kernels: [block][gdyn_stride] per-channel tables in HBM
+  size_t gdyn_stride;
 };
+
+// The per-channel tables a workgroup builds (Meta, the data pass's channel
+// phases and flags) live in dynamic LDS up to PPF_LDS_NCHAN channels.  The
+// WIDE instantiations, taken above that (or under PPF_OPT_HBM_TABLES), keep
+// them in the block's slice of an HBM workspace instead: the same values and
+// the same arithmetic, so the same fits, at any channel count up to
+// PPF_MAX_NCHAN.  Block-local data either way (written, block barrier, read).
+template <bool WIDE, class Args>
+__device__ __forceinline__ unsigned char* chan_tables(const Args& a, unsigned char* lds) {
+  if constexpr (WIDE) return a.gdyn + (size_t)blockIdx.x * a.gdyn_stride;
+  else return lds;
+}
 
 // Subint s fitted by the Taylor path (fused_taylor's test, on the data
 // pass's arguments): no scattering at the start and tau not fitted.
@@ -145,6 +159,8 @@ struct FitArgs {
   double* o_grad;            // [nsub][5] or null
   double* o_hess;            // [nsub][25] or null
   double bounds[5][2];       // TNC bounds (NaN = None)
+  unsigned char* gdyn;       // WIDE kernels: [block][gdyn_stride] per-channel tables in HBM
+  size_t gdyn_stride;
 };
 
 // One solver-trace record (diagnostic, ppf_set_trace): the point, f, the
@@ -723,7 +739,7 @@ __global__ void k_twiddles(double2* tw, int nbin);
 template <int LOGN>
 __global__ void k_model_spec(const double* model, double2* M, double* pn, int NHP, int zero_dc,
                              const double2* tw, double* M2);
-template <int LOGN> __global__ void k_data_xspec(SpecArgs a);
+template <int LOGN, bool WIDE = false> __global__ void k_data_xspec(SpecArgs a);
 template <int LOGN> __global__ void k_phase_shift(PhaseShiftArgs a);
 template <int LOGN>
 __global__ void k_rotate_rows(const double* in, const double* phase, const double* tau,
@@ -773,15 +789,15 @@ __host__ __device__ inline size_t scat_sweep_lds(int nchan, int split) {
 __global__ void k_scat_sweep(FitArgs a, double* part, int split, int init);
 __global__ void k_scat_step(FitArgs a, const double* part, int init, int* ctrs, int par);
 __global__ void k_model_mean(const double2* M, double2* Mmean, int nchan, int NHP);
-template <bool MOM, bool DSP>
+template <bool MOM, bool DSP, bool WIDE = false>
 __global__ void k_fit_taylor(FitArgs a);
 template <int U, bool DSP>
 __global__ void k_moments(FitArgs a);
 __global__ void k_selftest(int* fails);
-template <bool SCAT> __global__ void k_solve(FitArgs a);
-template <bool SCAT> __global__ void k_tnc(FitArgs a);
-template <bool SCAT> __global__ void k_ncg(FitArgs a);
+template <bool SCAT, bool WIDE = false> __global__ void k_solve(FitArgs a);
+template <bool SCAT, bool WIDE = false> __global__ void k_tnc(FitArgs a);
+template <bool SCAT, bool WIDE = false> __global__ void k_ncg(FitArgs a);
 __global__ void k_guess_w(FitArgs a);
-template <bool SCAT> __global__ void k_post(FitArgs a);
+template <bool SCAT, bool WIDE = false> __global__ void k_post(FitArgs a);
 
 }  // namespace ppf

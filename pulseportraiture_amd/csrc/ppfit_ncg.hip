@@ -421,7 +421,7 @@ __device__ bool wolfe2(Obj& O, const Line& L, double phi0, bool have_old, double
 }
 
 // _minimize_newtoncg (maxiter 2000, xtol -1, c1 1e-4, c2 0.9): status as scipy
-template <bool SCAT>
+template <bool SCAT, bool W>  // W: one copy per k_ncg instantiation (its only caller)
 __device__ int run(Obj& O, double* xk, double& fval) {
 #pragma clang fp contract(off)
   const double c1 = 1e-4, c2 = 0.9;
@@ -535,7 +535,7 @@ struct Shared {
 }  // namespace ncg
 
 // fit_portrait_full(method='Newton-CG') on one subint.
-template <bool SCAT>
+template <bool SCAT, bool WIDE>
 __global__ __launch_bounds__(kBlock, 1) void k_ncg(FitArgs a) {
   extern __shared__ __align__(16) unsigned char dyn[];
   __shared__ ncg::Shared sh;
@@ -543,7 +543,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_ncg(FitArgs a) {
   const int c = blockIdx.x, s = a.sub0 + c, tid = threadIdx.x;
   if (a.method != PPF_METHOD_NEWTON_CG) return;
   if ((a.st[c].scat != 0) != SCAT) return;  // the other variant owns this subint
-  const Meta m = load_meta(a, c, s, dyn, &sh.nok);
+  const Meta m = load_meta(a, c, s, chan_tables<WIDE>(a, dyn), &sh.nok);
   SolveState& st = a.st[c];
   if (tid < 3) refs[tid] = st.refs[tid];
   __syncthreads();
@@ -566,7 +566,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_ncg(FitArgs a) {
   int status = -1;
   double f = NAN;
   if (m.nok > 0) {
-    status = ncg::run<SCAT>(O, x, f);
+    status = ncg::run<SCAT, WIDE>(O, x, f);
     // k_post reads the per-channel sums of x from acc slot 0: refresh them
     // when the last sweep was a rejected trial point (scipy does not
     // evaluate there: not counted)
@@ -585,7 +585,9 @@ __global__ __launch_bounds__(kBlock, 1) void k_ncg(FitArgs a) {
   }
 }
 
-template __global__ void k_ncg<false>(FitArgs);
-template __global__ void k_ncg<true>(FitArgs);
+template __global__ void k_ncg<false, false>(FitArgs);
+template __global__ void k_ncg<true, false>(FitArgs);
+template __global__ void k_ncg<false, true>(FitArgs);
+template __global__ void k_ncg<true, true>(FitArgs);
 
 }  // namespace ppf

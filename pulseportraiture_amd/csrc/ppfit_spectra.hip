@@ -106,7 +106,7 @@ inline size_t xspec_dyn_lds(int nchan) {
   return (size_t)nchan * sizeof(double2) + (((size_t)nchan + 15) & ~(size_t)15);
 }
 
-template <int LOGN>
+template <int LOGN, bool WIDE>
 __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
   using Cfg = XspecCfg<LOGN>;
   constexpr int N = Cfg::N;
@@ -126,8 +126,9 @@ __global__ __launch_bounds__(kBlock, 2) void k_data_xspec(SpecArgs a) {
   __shared__ double s_meta[4];
   __shared__ int s_act[WPB];
   extern __shared__ __align__(16) unsigned char dyn[];
-  double2* cmeta = reinterpret_cast<double2*>(dyn);  // (phi_g, weight or NaN if masked)
-  uint8_t* cact = dyn + (size_t)a.nchan * sizeof(double2);  // fitted channel flags
+  unsigned char* ctab = chan_tables<WIDE>(a, dyn);
+  double2* cmeta = reinterpret_cast<double2*>(ctab);  // (phi_g, weight or NaN if masked)
+  uint8_t* cact = ctab + (size_t)a.nchan * sizeof(double2);  // fitted channel flags
   const int c = blockIdx.x;
   const int s = a.sub0 + c;
   const bool tsub = a.D && spec_taylor_sub(a, s);
@@ -922,7 +923,8 @@ __global__ __launch_bounds__(kBlock) void k_resid_chi2(ResidArgs a, const double
 #define PPF_INST(L)                                                                          \
   template __global__ void k_model_spec<L>(const double*, double2*, double*, int, int,       \
                                            const double2*, double*);                         \
-  template __global__ void k_data_xspec<L>(SpecArgs);                                        \
+  template __global__ void k_data_xspec<L, false>(SpecArgs);                                 \
+  template __global__ void k_data_xspec<L, true>(SpecArgs);                                  \
   template __global__ void k_phase_shift<L>(PhaseShiftArgs);                                 \
   template __global__ void k_rotate_rows<L>(const double*, const double*, const double*,     \
                                             double*, const double2*);                        \

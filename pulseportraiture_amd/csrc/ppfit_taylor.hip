@@ -399,7 +399,7 @@ __device__ __forceinline__ double wave_reach(const Meta& m, double p0, double p1
 // one subint with the latency-bound trust-region iterations of another
 // (measured: 9.26 -> 9.03 ms per headline step; fusing the post-fit too
 // spilled 784 B per lane and was slower, 10.0 ms).
-template <bool MOM, bool DSP>
+template <bool MOM, bool DSP, bool WIDE>
 __global__ __launch_bounds__(kBlock, 3) void k_fit_taylor(FitArgs a) {
   extern __shared__ __align__(16) unsigned char dyn[];
   __shared__ TaylorShared sh;
@@ -435,7 +435,7 @@ __global__ __launch_bounds__(kBlock, 3) void k_fit_taylor(FitArgs a) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   }
   mark(0);  // slot 0: the fused first moment pass
-  unsigned char* dmeta = dyn;
+  unsigned char* dmeta = chan_tables<WIDE>(a, dyn);
   SolveState& st = a.st[c];
   // T slot 0 (k_moments) read once into LDS: every sweep about centre 0 then
   // reads LDS instead of HBM.  load_meta's barrier publishes it.
@@ -664,6 +664,10 @@ template __global__ void k_fit_taylor<false, false>(FitArgs);
 template __global__ void k_fit_taylor<true, false>(FitArgs);
 template __global__ void k_fit_taylor<false, true>(FitArgs);
 template __global__ void k_fit_taylor<true, true>(FitArgs);
+template __global__ void k_fit_taylor<false, false, true>(FitArgs);
+template __global__ void k_fit_taylor<true, false, true>(FitArgs);
+template __global__ void k_fit_taylor<false, true, true>(FitArgs);
+template __global__ void k_fit_taylor<true, true, true>(FitArgs);
 
 // ---------------------------------------------------------------------------
 // Device self-test of the cross-lane primitives (DPP, permlane swaps,

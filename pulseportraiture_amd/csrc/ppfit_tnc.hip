@@ -349,7 +349,7 @@ struct TncShared {
   int nok;
 };
 
-template <bool SCAT>
+template <bool SCAT, bool W>  // W: one copy per k_tnc instantiation (its only caller)
 __device__ int tnc_run(TncState& T, TncObjective& O, double* x, double& f_out, double fmin,
                        double xtol) {
 #pragma clang fp contract(off)
@@ -873,7 +873,7 @@ __device__ int tnc_run(TncState& T, TncObjective& O, double* x, double& f_out, d
 }
 
 // fit_portrait_full(method='TNC') / legacy fit_portrait on one subint.
-template <bool SCAT>
+template <bool SCAT, bool WIDE>
 __global__ __launch_bounds__(kBlock, 1) void k_tnc(FitArgs a) {
   extern __shared__ __align__(16) unsigned char dyn[];
   __shared__ TncShared sh;
@@ -881,7 +881,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_tnc(FitArgs a) {
   const int c = blockIdx.x, s = a.sub0 + c, tid = threadIdx.x;
   if (a.method != PPF_METHOD_TNC && a.method != PPF_METHOD_TNC_LEGACY) return;
   if ((a.st[c].scat != 0) != SCAT) return;  // the other variant owns this subint
-  const Meta m = load_meta(a, c, s, dyn, &sh.nok);
+  const Meta m = load_meta(a, c, s, chan_tables<WIDE>(a, dyn), &sh.nok);
   SolveState& st = a.st[c];
   const double P = a.P[s];
   if (tid < 3) refs[tid] = st.refs[tid];
@@ -936,7 +936,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_tnc(FitArgs a) {
       T.xscale[i] = 1.0;
       T.xoffset[i] = 0.0;
     }
-    status = tnc_run<SCAT>(T, O, x, f, fmin, 1e-10);
+    status = tnc_run<SCAT, WIDE>(T, O, x, f, fmin, 1e-10);
     // scipy's _minimize_tnc ends with func_and_grad(x): the result's fun and
     // jac, and one more nfev when x is not the last evaluated point.  Every
     // sweep writes acc slot 0, so it then holds x's per-channel sums (k_post).
@@ -957,7 +957,9 @@ __global__ __launch_bounds__(kBlock, 1) void k_tnc(FitArgs a) {
   }
 }
 
-template __global__ void k_tnc<false>(FitArgs);
-template __global__ void k_tnc<true>(FitArgs);
+template __global__ void k_tnc<false, false>(FitArgs);
+template __global__ void k_tnc<true, false>(FitArgs);
+template __global__ void k_tnc<false, true>(FitArgs);
+template __global__ void k_tnc<true, true>(FitArgs);
 
 }  // namespace ppf
