@@ -19,6 +19,8 @@ Two kinds of check:
 - nchan = 2112 and 4096 (above the LDS limit) against the oracle, at the
   north_star tolerance (|dphi| <= 1e-3 sigma_phi, |dDM| <= 1e-3 sigma_DM)
   with identical solver status.
+- get_TOAs end to end on a 2,304-channel archive whose last 256 channels
+  are zapped: the same TOAs and .tim text as the 2,048-channel archive.
 """
 import numpy as np
 import pytest
@@ -166,3 +168,66 @@ def test_nchan_limit(eng):
     with pytest.raises(PPFitError, match="nchan"):
         eng.fit_batch(data, np.zeros((16385, 64)), np.linspace(1000, 2000, 16385), w.P,
                       np.zeros(5), [1, 1, 0, 0, 0])
+
+
+def test_get_toas_zapped_extra_channels(tmp_path):
+    """get_TOAs end to end above the LDS limit: an archive of 2,304 channels
+    whose last 256 carry zero weight gives the TOAs, errors, scales and .tim
+    text of the same archive cut to its 2,048 weighted channels (the
+    reference fits ok_ichans only, pptoas.py:343-364) -- the first on the
+    HBM-table kernels, the second on the LDS ones."""
+    import os
+    import re
+    import shutil
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from pulseportraiture_amd import archive, pplib, pptoas
+    from tests.golden_consts import DM0
+    nsub, nchan, extra, nbin = 4, 2048, 256, 256
+    w = synth.make_workload(nsub, nchan, nbin, seed=630)
+    data = synth.workload_data_host(w)
+    rng = np.random.default_rng(631)
+    df = w.freqs[1] - w.freqs[0]
+    freqs_x = np.concatenate([w.freqs, w.freqs[-1] + df * np.arange(1, extra + 1)])
+    data_x = np.concatenate([data, rng.standard_normal((nsub, extra, nbin))], axis=1)
+    weights_x = np.ones((nsub, nchan + extra))
+    weights_x[:, nchan:] = 0.0
+    common = dict(Ps=np.full(nsub, w.P), epochs=[(57200 + k, 0, 0.0) for k in range(nsub)],
+                  DM=DM0, nu0=1500.0, dmc=0)
+    archive.register_archive("cut", dict(subints=data[:, None], freqs=w.freqs,
+                                         weights=np.ones((nsub, nchan)), **common))
+    archive.register_archive("wide", dict(subints=data_x[:, None], freqs=freqs_x,
+                                          weights=weights_x, **common))
+    shutil.copy(synth.EXAMPLE_GMODEL, str(tmp_path / "example.gmodel"))
+    cwd = os.getcwd()
+    os.chdir(tmp_path)
+    try:
+        gts, tims = [], []
+        for name in ("cut", "wide"):
+            gt = pptoas.GetTOAs([name], "example.gmodel", quiet=True)
+            gt.get_TOAs(quiet=True)
+            tim = str(tmp_path / (name + ".tim"))
+            pplib.write_TOAs(gt.TOA_list, SNR_cutoff=0.0, outfile=tim, append=False)
+            gts.append(gt)
+            # -nch counts the zapped channels too (pptoas.py:633, nchan);
+            # every other flag, -nchx and -bw included, is over ok channels
+            txt = re.sub(r" -nch \d+", "", open(tim).read())
+            tims.append(re.sub(r"(?m)^wide ", "cut ", txt))
+    finally:
+        os.chdir(cwd)
+        archive.unregister_archive("cut")
+        archive.unregister_archive("wide")
+    cut, wide = gts
+    for attr in ("phis", "phi_errs", "DMs", "DM_errs", "snrs", "red_chi2s", "covariances",
+                 "nfevals", "rcs", "nu_refs", "TOA_errs"):
+        a = np.asarray(getattr(cut, attr)[0], dtype=np.float64)
+        b = np.asarray(getattr(wide, attr)[0], dtype=np.float64)
+        assert np.array_equal(a, b, equal_nan=True), attr
+    for attr in ("scales", "scale_errs", "channel_snrs"):
+        a = np.asarray(getattr(cut, attr)[0])
+        b = np.asarray(getattr(wide, attr)[0])
+        assert b.shape[-1] == nchan + extra, attr
+        assert np.array_equal(a, b[..., :nchan]), attr
+        assert np.all(b[..., nchan:] == 0.0), attr
+    assert tims[0] == tims[1]
