@@ -44,13 +44,19 @@
  *    trust-ncg codes (0 gradient small / NaN, 1 maxiter, 2 no predicted
  *    reduction, 3 linalg error), as returned by the reference's
  *    results.status (pptoaslib.py:1018).
- *  - Shapes the reference accepts and this library refuses (PPF_ERR_INVALID
- *    with a message, never a silent fallback): nbin must be a power of two
- *    in [64, 8192] (the register / LDS FFTs and the Taylor power tables are
- *    built per power of two; the reference's numpy rfft takes any length,
- *    pptoaslib.py:976-978), and nchan <= PPF_MAX_NCHAN (the reference
- *    takes any channel count; 16384 covers every receiver in use).  A caller
- *    with another nbin must resample; there is no generic-length path.
+ *  - Shapes (PPF_ERR_UNSUPPORTED with a message outside them, never a
+ *    silent fallback): nbin in [64, 8192] and nchan <= PPF_MAX_NCHAN (the
+ *    reference takes any; 16384 channels covers every receiver in use).
+ *    The FFT kernels are built per power of two; for any other nbin (the
+ *    reference's numpy rfft takes any length, pptoaslib.py:976-978)
+ *    ppf_fit_portrait_batch, ppf_rotate_rows, ppf_scatter_rotate_rows and
+ *    ppf_gaussian_portraits run direct-sum kernels instead (O(nbin^2) per
+ *    row; tests/test_gpu_generic_nbin.py), and the data-spectrum cache
+ *    (PPF_SPEC_*, ppf_spec_nhp) and the other row entry points
+ *    (ppf_phase_shift_batch, ppf_rotate_accumulate*, ppf_irfft_rows,
+ *    ppf_noise_rows, ppf_resid_chi2_rows, ppf_synth_portraits,
+ *    ppf_spline_portraits, ppf_instrumental_response_rows) still take powers
+ *    of two only.
  *  - Channel counts: up to PPF_LDS_NCHAN a fit workgroup keeps its subint's
  *    per-channel tables (frequencies, weights, dispersion derivatives, the
  *    fitted-channel list) in LDS; above it (or under PPF_OPT_HBM_TABLES) the

@@ -24,7 +24,7 @@ CXX = os.environ.get("CXX", "g++")
 
 SOURCES = ["ppfit_lib.hip"]
 DEPS = ["ppfit_lib.hip", "ppfit_spectra.hip", "ppfit_fit.hip", "ppfit_taylor.hip", "ppfit_tnc.hip",
-        "ppfit_ncg.hip", "ppfit_models.hip", "ppfit_capi.hip", "ppfit_kernels.hpp",
+        "ppfit_ncg.hip", "ppfit_models.hip", "ppfit_generic.hip", "ppfit_capi.hip", "ppfit_kernels.hpp",
         "ppfit_device.hpp"]
 OUT = os.path.join(HERE, "libppfit.so")
 FITS_OUT = os.path.join(HERE, "libppfits.so")

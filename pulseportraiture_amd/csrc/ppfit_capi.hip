@@ -45,6 +45,8 @@ struct ppf_ctx {
   int64_t ws_limit = (int64_t)32 << 30;
   double2* tw[16] = {nullptr};
   double2* vp[16] = {nullptr};  // moment power tables (k_vpow)
+  // the same two tables for nbin that are not powers of two
+  std::vector<std::pair<int, double2*>> tw_gen, vp_gen;
   Buffer ws;     // per-chunk fit workspace
   Buffer mspec;   // template spectra
   Buffer aux;     // misc (synth templates, partial sums)
@@ -103,6 +105,37 @@ int check_nbin(ppf_ctx* ctx, int nbin, int* logN) {
   return PPF_OK;
 }
 
+// Entry points with a generic-length path (ppfit_generic.hip): any nbin in
+// [64, 8192]; *logN = -1 when nbin is not a power of two.
+int check_nbin_any(ppf_ctx* ctx, int nbin, int* logN) {
+  if (nbin < 64 || nbin > 8192)
+    return fail(ctx, PPF_ERR_UNSUPPORTED, "nbin=%d: outside [64, 8192]", nbin);
+  const int l = ilog2_exact(nbin);
+  *logN = l < 0 ? -1 : l - 1;
+  return PPF_OK;
+}
+
+// dynamic LDS of the generic-length kernels
+size_t gen_row_lds(int nbin) { return (size_t)nbin * sizeof(double); }
+size_t gen_rot_lds(int nbin) {
+  return (((size_t)nbin * sizeof(double) + 15) & ~(size_t)15) + (size_t)(nbin / 2 + 1) * sizeof(double2);
+}
+
+// the table of nbin in a generic-length cache (created by make on first use)
+template <typename F>
+int gen_table(ppf_ctx* ctx, std::vector<std::pair<int, double2*>>& cache, int nbin, size_t n,
+              F&& make, const double2** out) {
+  for (auto& p : cache)
+    if (p.first == nbin) { *out = p.second; return PPF_OK; }
+  double2* t = nullptr;
+  HIPCHK(ctx, hipMalloc(&t, n * sizeof(double2)));
+  cache.push_back({nbin, t});
+  make(t);
+  HIPCHK(ctx, hipGetLastError());
+  *out = t;
+  return PPF_OK;
+}
+
 // rows of 16 cells (256 B): measured faster than 8 or 32
 int nharm_pad(int nbin) { return ((nbin / 2 + 1) + 15) & ~15; }
 
@@ -125,6 +158,10 @@ int ensure(ppf_ctx* ctx, Buffer& b, size_t bytes) {
 
 int twiddles(ppf_ctx* ctx, int nbin, const double2** out) {
   const int l = ilog2_exact(nbin);
+  if (l < 0)
+    return gen_table(ctx, ctx->tw_gen, nbin, (size_t)nbin, [&](double2* t) {
+      hipLaunchKernelGGL(k_twiddles, dim3((nbin + 255) / 256), dim3(256), 0, ctx->stream, t, nbin);
+    }, out);
   if (!ctx->tw[l]) {
     HIPCHK(ctx, hipMalloc(&ctx->tw[l], (size_t)nbin * sizeof(double2)));
     hipLaunchKernelGGL(k_twiddles, dim3((nbin + 255) / 256), dim3(256), 0, ctx->stream,
@@ -163,11 +200,16 @@ int taylor_lds_moments(int nchan, size_t lds_meta) {
 
 int vpow_table(ppf_ctx* ctx, int nbin, const double2** out) {
   const int l = ilog2_exact(nbin);
+  const int rows = kVpowRows(nbin / 2);
+  if (l < 0)
+    return gen_table(ctx, ctx->vp_gen, nbin, (size_t)rows * 16, [&](double2* t) {
+      hipLaunchKernelGGL(k_vpow, dim3((rows * 16 + 255) / 256), dim3(256), 0, ctx->stream, t,
+                         nbin, rows);
+    }, out);
   if (!ctx->vp[l]) {
-    const int rows = kVpowRows(nbin / 2);
     HIPCHK(ctx, hipMalloc(&ctx->vp[l], (size_t)rows * 16 * sizeof(double2)));
     hipLaunchKernelGGL(k_vpow, dim3((rows * 16 + 255) / 256), dim3(256), 0, ctx->stream,
-                       ctx->vp[l], nbin / 2, rows);
+                       ctx->vp[l], nbin, rows);
     HIPCHK(ctx, hipGetLastError());
   }
   *out = ctx->vp[l];
@@ -258,7 +300,7 @@ int resolve_timing(ppf_ctx* ctx) {
 int model_spectra(ppf_ctx* ctx, int nrow, int nbin, const double* model, int zero_dc, Buffer& buf,
                   double2** M, double** pn, double** M2 = nullptr) {
   int logN;
-  if (int r = check_nbin(ctx, nbin, &logN)) return r;
+  if (int r = check_nbin_any(ctx, nbin, &logN)) return r;
   const int NHP = nharm_pad(nbin);
   const size_t mbytes = (size_t)nrow * NHP * sizeof(double2);
   const size_t pbytes = ((size_t)nrow * sizeof(double) + 255) & ~(size_t)255;
@@ -273,6 +315,9 @@ int model_spectra(ppf_ctx* ctx, int nrow, int nbin, const double* model, int zer
   double2* Mp = *M;
   double* pp = *pn;
   return timed(ctx, PPF_K_MODEL_FFT, [&] {
+    if (logN < 0)
+      hipLaunchKernelGGL(k_model_spec_gen, dim3(nrow), dim3(kBlock), gen_row_lds(nbin),
+                         ctx->stream, model, Mp, pp, NHP, zero_dc, tw, m2p, nbin);
     LOGN_SWITCH(logN, hipLaunchKernelGGL(k_model_spec<LG>, dim3(nrow), dim3(kBlock), 0,
                                          ctx->stream, model, Mp, pp, NHP, zero_dc, tw, m2p));
   });
@@ -333,6 +378,8 @@ void ppf_ctx_destroy(ppf_ctx* ctx) {
   }
   for (auto p : ctx->tw) if (p) (void)hipFree(p);
   for (auto p : ctx->vp) if (p) (void)hipFree(p);
+  for (auto& p : ctx->tw_gen) (void)hipFree(p.second);
+  for (auto& p : ctx->vp_gen) (void)hipFree(p.second);
   if (ctx->ptime.p) (void)hipFree(ctx->ptime.p);
   if (ctx->spart.p) (void)hipFree(ctx->spart.p);
   if (ctx->tmpl.p) (void)hipFree(ctx->tmpl.p);
@@ -439,7 +486,9 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
     return fail(ctx, PPF_ERR_INVALID, "missing required output pointer");
   if (d->guess && d->guess_Ns < 2) return fail(ctx, PPF_ERR_INVALID, "guess_Ns must be >= 2");
   int logN;
-  if (int r = check_nbin(ctx, d->nbin, &logN)) return r;
+  // nbin not a power of two: the generic-length data pass and template
+  // spectra (ppfit_generic.hip); every solver kernel takes any nbin
+  if (int r = check_nbin_any(ctx, d->nbin, &logN)) return r;
   HIPCHK(ctx, hipSetDevice(ctx->device));
   const int nchan = d->nchan, nbin = d->nbin;
   const int NH = nbin / 2 + 1, NHP = nharm_pad(nbin);
@@ -469,6 +518,9 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
     if (!taylor || d->fit_flags[3] || d->fit_flags[4])
       return fail(ctx, PPF_ERR_UNSUPPORTED, "the data-spectrum cache takes phase-family "
                   "trust-ncg fits only (tau and alpha not fitted, not PPF_SOLVE_EXACT)");
+    if (logN < 0)
+      return fail(ctx, PPF_ERR_UNSUPPORTED, "the data-spectrum cache needs a power-of-two nbin "
+                  "(nbin=%d)", d->nbin);
   }
   // mean template spectrum for the unmasked guess
   double2* Mmean = nullptr;
@@ -693,6 +745,9 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
         bind_spec(sp, fp, s0 + off);
         if (prev_x) HIPCHK(ctx, hipStreamWaitEvent(st, prev_x, 0));
         if (int r = timed_on(ctx, PPF_K_DATA_XSPEC, st, [&] {
+              if (logN < 0)
+                hipLaunchKernelGGL(k_data_xspec_gen, dim3(n), dim3(kBlock), gen_row_lds(nbin), st,
+                                   sp, nbin);
               LOGN_SWITCH(logN, WIDE_SWITCH(wide, hipLaunchKernelGGL((k_data_xspec<LG, WD>), dim3(n),
                                                    dim3(XspecCfg<LG>::WPB * 64),
                                                    lds_xspec, st, sp)));
@@ -750,6 +805,9 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
     fa.sub0 = (int)s0;
     bind_spec(sa, fa, s0);
     if (int r = timed(ctx, PPF_K_DATA_XSPEC, [&] {
+          if (logN < 0)
+            hipLaunchKernelGGL(k_data_xspec_gen, dim3(nc), dim3(kBlock), gen_row_lds(nbin),
+                               ctx->stream, sa, nbin);
           LOGN_SWITCH(logN, WIDE_SWITCH(wide, hipLaunchKernelGGL((k_data_xspec<LG, WD>), dim3(nc),
                                                                  dim3(XspecCfg<LG>::WPB * 64),
                                                                  lds_xspec, ctx->stream, sa)));
@@ -995,11 +1053,14 @@ int ppf_rotate_rows(ppf_ctx* ctx, int32_t nrow, int32_t nbin, const double* in,
   if (!ctx || !in || !phase || !out) return fail(ctx, PPF_ERR_INVALID, "null argument");
   if (nrow <= 0) return PPF_OK;
   int logN;
-  if (int r = check_nbin(ctx, nbin, &logN)) return r;
+  if (int r = check_nbin_any(ctx, nbin, &logN)) return r;
   HIPCHK(ctx, hipSetDevice(ctx->device));
   const double2* tw;
   if (int r = twiddles(ctx, nbin, &tw)) return r;
   return timed(ctx, PPF_K_ROTATE, [&] {
+    if (logN < 0)
+      hipLaunchKernelGGL(k_rotate_rows_gen, dim3(nrow), dim3(kBlock), gen_rot_lds(nbin),
+                         ctx->stream, in, phase, nullptr, out, tw, nbin);
     LOGN_SWITCH(logN, hipLaunchKernelGGL(k_rotate_rows<LG>, dim3(nrow), dim3(kBlock), 0,
                                          ctx->stream, in, phase, nullptr, out, tw));
   });
@@ -1010,12 +1071,15 @@ int ppf_scatter_rotate_rows(ppf_ctx* ctx, int32_t nrow, int32_t nbin, const doub
   if (!ctx || !in || !out) return fail(ctx, PPF_ERR_INVALID, "null argument");
   if (nrow <= 0) return PPF_OK;
   int logN;
-  if (int r = check_nbin(ctx, nbin, &logN)) return r;
+  if (int r = check_nbin_any(ctx, nbin, &logN)) return r;
   HIPCHK(ctx, hipSetDevice(ctx->device));
   const double2* tw;
   if (int r = twiddles(ctx, nbin, &tw)) return r;
   if (!phase) return fail(ctx, PPF_ERR_INVALID, "phase must be given (zeros for none)");
   return timed(ctx, PPF_K_ROTATE, [&] {
+    if (logN < 0)
+      hipLaunchKernelGGL(k_rotate_rows_gen, dim3(nrow), dim3(kBlock), gen_rot_lds(nbin),
+                         ctx->stream, in, phase, tau, out, tw, nbin);
     LOGN_SWITCH(logN, hipLaunchKernelGGL(k_rotate_rows<LG>, dim3(nrow), dim3(kBlock), 0,
                                          ctx->stream, in, phase, tau, out, tw));
   });
@@ -1303,7 +1367,7 @@ int ppf_gaussian_portraits(ppf_ctx* ctx, int32_t nrow, int32_t nbin, int32_t nga
     if (code[i] != 0 && code[i] != 1)
       return fail(ctx, PPF_ERR_INVALID, "model code digit %d: 0 (power law) or 1 (linear)", code[i]);
   int logN;
-  if (int r = check_nbin(ctx, nbin, &logN)) return r;
+  if (int r = check_nbin_any(ctx, nbin, &logN)) return r;
   HIPCHK(ctx, hipSetDevice(ctx->device));
   GaussArgs g;
   g.nbin = nbin;
@@ -1336,6 +1400,9 @@ int ppf_gaussian_portraits(ppf_ctx* ctx, int32_t nrow, int32_t nbin, int32_t nga
   return timed(ctx, PPF_K_MODEL_FFT, [&] {
     hipLaunchKernelGGL(k_scat_taus, dim3((nrow + 255) / 256), dim3(256), 0, ctx->stream, freqs,
                        nrow, params[1] / (double)nbin, alpha, nu_ref, taus);
+    if (logN < 0)
+      hipLaunchKernelGGL(k_rotate_rows_gen, dim3(nrow), dim3(kBlock), gen_rot_lds(nbin),
+                         ctx->stream, rows, nullptr, taus, out, tw, nbin);
     LOGN_SWITCH(logN, hipLaunchKernelGGL(k_rotate_rows<LG>, dim3(nrow), dim3(kBlock), 0,
                                          ctx->stream, rows, nullptr, taus, out, tw));
   });

@@ -1,0 +1,228 @@
+// ppfit_generic.hip -- rfft-based kernels of libppfit for any nbin (gfx950).
+//
+// The reference transforms profiles with numpy's rfft / irfft of whatever
+// length the archive has (pptoaslib.py:976-978, pplib.py:2338-2426).  The
+// register and LDS FFTs of ppfit_spectra.hip are built per power of two; for
+// every other nbin in [64, 8192] these kernels take their place in the fit
+// entry point, the template spectra and the row rotations: the same outputs
+// (the spectra's layout, X, sig, dsum, R, rotated rows) from direct sums,
+// O(nbin^2) per row instead of O(nbin log nbin).
+//
+// Bin k of a real row: D_k = sum_m x_m e^{-2 pi i m k / nbin}.  The phasor
+// advances by one complex product per term and is re-seeded from the twiddle
+// table at the exact index (m k) mod nbin every kSeed terms, so its rounding
+// never grows past kSeed products (relative error ~1e-15, against the
+// north_star tolerance of 1e-3 sigma on the fitted parameters).
+#include "ppfit_kernels.hpp"
+
+namespace ppf {
+
+constexpr int kSeed = 32;
+
+// D_k of x[0 .. nbin) (LDS); tw[j] = e^{-2 pi i j / nbin}, k < nbin
+__device__ __forceinline__ double2 dft_bin(const double* x, int nbin, int k,
+                                           const double2* __restrict__ tw) {
+  const double2 w = tw[k];
+  const int step = (int)(((long long)kSeed * k) % nbin);
+  double re = 0.0, im = 0.0;
+  int seed = 0;  // (m0 k) mod nbin
+  for (int m0 = 0; m0 < nbin; m0 += kSeed) {
+    double2 e = tw[seed];
+    const int me = min(m0 + kSeed, nbin);
+    for (int m = m0; m < me; ++m) {
+      const double v = x[m];
+      re = fma(v, e.x, re);
+      im = fma(v, e.y, im);
+      e = cmul(e, w);
+    }
+    seed += step;
+    if (seed >= nbin) seed -= nbin;
+  }
+  return cmk(re, im);
+}
+
+// numpy irfft(X, n = nbin) at sample m: (Re X_0 + 2 sum_{1 <= k <= K} Re(X_k
+// e^{2 pi i m k / nbin}) + [nbin even] Re X_{nbin/2} (-1)^m) / nbin, K = (nbin - 1) / 2;
+// X[0 .. nbin/2] in LDS
+__device__ __forceinline__ double idft_sample(const double2* X, int nbin, int m,
+                                              const double2* __restrict__ tw) {
+  const double2 w = cconj(tw[m]);  // e^{+2 pi i m / nbin}
+  const int K = (nbin - 1) / 2;
+  const int step = (int)(((long long)kSeed * m) % nbin);
+  double acc = 0.0;
+  int seed = m;  // (k0 m) mod nbin at k0 = 1
+  for (int k0 = 1; k0 <= K; k0 += kSeed) {
+    double2 e = cconj(tw[seed]);
+    const int ke = min(k0 + kSeed - 1, K);
+    for (int k = k0; k <= ke; ++k) {
+      const double2 x = X[k];
+      acc = fma(x.x, e.x, acc);
+      acc = fma(-x.y, e.y, acc);
+      e = cmul(e, w);
+    }
+    seed += step;
+    if (seed >= nbin) seed -= nbin;
+  }
+  double v = fma(2.0, acc, X[0].x);
+  if (!(nbin & 1)) v += (m & 1) ? -X[nbin / 2].x : X[nbin / 2].x;
+  return v / (double)nbin;
+}
+
+__device__ __forceinline__ void load_real_row(double* x, const double* __restrict__ row, int nbin) {
+  for (int m = threadIdx.x; m < nbin; m += blockDim.x) x[m] = row[m];
+}
+
+// k_model_spec for any nbin: M[row][k], k <= nbin/2 (DC zeroed when
+// zero_dc), zero padding up to NHP, p_n = sum_{k>=1} |M_k|^2, |M_k|^2 rows.
+// Dynamic LDS: nbin doubles.
+__global__ __launch_bounds__(kBlock) void k_model_spec_gen(const double* __restrict__ model,
+                                                           double2* __restrict__ M,
+                                                           double* __restrict__ pn, int NHP,
+                                                           int zero_dc,
+                                                           const double2* __restrict__ tw,
+                                                           double* __restrict__ M2, int nbin) {
+  extern __shared__ __align__(16) unsigned char gsm[];
+  double* x = reinterpret_cast<double*>(gsm);
+  __shared__ double red[kWaves];
+  const int row = blockIdx.x, NH = nbin / 2 + 1;
+  load_real_row(x, model + (size_t)row * nbin, nbin);
+  __syncthreads();
+  double p = 0.0;
+  double2* out = M + (size_t)row * NHP;
+  for (int k = threadIdx.x; k < NHP; k += kBlock) {
+    double2 v = cmk(0.0, 0.0);
+    if (k < NH) v = dft_bin(x, nbin, k, tw);
+    if (k == 0 && zero_dc) v = cmk(0.0, 0.0);
+    if (k >= 1 && k < NH) p += cabs2(v);
+    out[k] = v;
+    if (M2) M2[(size_t)row * NHP + k] = cabs2(v);
+  }
+  p = block_sum(p, red);
+  if (threadIdx.x == 0 && pn) pn[row] = p;
+}
+
+// k_data_xspec for any nbin: one workgroup per subint, its channel rows in
+// order.  Per fitted channel: D = rfft(row); sig = errs or get_noise_PS
+// (pplib.py:2227-2253); dsum = sum_{k>=1} |D_k|^2; X_k = D_k conj(M_k) (0 at
+// k = 0); R_k += w_n D_k e^{2 pi i k phi_n} (the guess's dedispersed, weighted
+// average, pptoas.py:421-423), each R_k summed by one thread in channel order.
+// Masked channels: sig = dsum = 0 and a zero X row.  No data-spectrum cache
+// (the entry point refuses PPF_SPEC_* for these lengths).  Dynamic LDS: nbin
+// doubles.
+__global__ __launch_bounds__(kBlock) void k_data_xspec_gen(SpecArgs a, int nbin) {
+  extern __shared__ __align__(16) unsigned char gsm[];
+  double* x = reinterpret_cast<double*>(gsm);
+  __shared__ double s_meta[4];
+  __shared__ double red[kWaves];
+  const int c = blockIdx.x, s = a.sub0 + c, tid = threadIdx.x;
+  const int nchan = a.nchan, NH = nbin / 2 + 1;
+  const double* fr = a.freqs + (size_t)s * nchan;
+  const uint8_t* mask = a.mask ? a.mask + (size_t)s * nchan : nullptr;
+  // nu_g (guess dedispersion reference): mean over fitted channels unless given
+  if (tid == 0) {
+    double fs = 0.0, ws = 0.0;
+    int nok = 0;
+    for (int q = 0; q < nchan; ++q) {
+      if (mask && !mask[q]) continue;
+      fs += fr[q];
+      ws += a.weights ? a.weights[(size_t)s * nchan + q] : 1.0;
+      ++nok;
+    }
+    double nug = a.guess_nu ? a.guess_nu[s] : NAN;
+    if (isnan(nug)) nug = fs / nok;
+    s_meta[0] = nug;
+    s_meta[1] = ws;
+    s_meta[2] = (double)nok;
+    s_meta[3] = a.init ? a.init[(size_t)s * 5 + 1] : 0.0;
+  }
+  __syncthreads();
+  const double nug2 = 1.0 / (s_meta[0] * s_meta[0]);
+  const double wsum = s_meta[1];
+  const double Dfac = kDconst * s_meta[3] / a.P[s];
+  const int midx = a.model_idx ? a.model_idx[s] : 0;
+  double2* Rr = a.R + (size_t)c * a.NHP;
+  if (a.guess)
+    for (int k = tid; k < a.NHP; k += kBlock) Rr[k] = cmk(0.0, 0.0);
+  for (int n = 0; n < nchan; ++n) {
+    double2* Xr = a.X + ((size_t)c * nchan + n) * a.NHP;
+    if (mask && !mask[n]) {
+      if (tid == 0) { a.sig[(size_t)c * nchan + n] = 0.0; a.dsum[(size_t)c * nchan + n] = 0.0; }
+      for (int k = tid; k < a.NHP; k += kBlock) Xr[k] = cmk(0.0, 0.0);
+      continue;
+    }
+    __syncthreads();  // the previous row's readers are done with x
+    load_real_row(x, a.data + ((size_t)s * nchan + n) * nbin, nbin);
+    __syncthreads();
+    const double2* Mr = a.M + ((size_t)midx * nchan + n) * a.NHP;
+    const double phi = Dfac * (1.0 / (fr[n] * fr[n]) - nug2);
+    const double wq = a.weights ? a.weights[(size_t)s * nchan + n] : 1.0;
+    double pn = 0.0, pd = 0.0;
+    for (int k = tid; k < a.NHP; k += kBlock) {
+      double2 xk = cmk(0.0, 0.0);
+      if (k < NH) {
+        const double2 d = dft_bin(x, nbin, k, a.tw);
+        const double p2 = cabs2(d);
+        if (k >= a.kc) pn += p2;
+        if (k >= 1) pd += p2;
+        if (k >= 1) xk = cmulc(d, Mr[k]);
+        if (a.guess) Rr[k] = cadd(Rr[k], cmul(d, cscale(turn_phasor((double)k, phi), wq)));
+      }
+      Xr[k] = xk;
+    }
+    pn = block_sum(pn, red);
+    pd = block_sum(pd, red);
+    if (tid == 0) {
+      double sig = a.errs ? a.errs[(size_t)s * nchan + n] : NAN;
+      if (isnan(sig)) sig = sqrt(pn / (double)nbin / (double)(NH - a.kc));
+      a.sig[(size_t)c * nchan + n] = sig;
+      a.dsum[(size_t)c * nchan + n] = pd;
+    }
+  }
+  if (a.guess) {
+    const double iw = 1.0 / wsum;
+    for (int k = tid; k < a.NHP; k += kBlock) {
+      double2 r = cmk(0.0, 0.0);
+      if (k < NH) {
+        r = cscale(Rr[k], iw);  // summed by this same thread
+        if (k == 0) r = cmk(0.0, 0.0);
+        if (!(nbin & 1) && k == nbin / 2) r.y = 0.0;  // irfft drops Im(X_N)
+      }
+      Rr[k] = r;
+    }
+  }
+}
+
+// k_rotate_rows for any nbin: rfft, times e^{2 pi i k phase} (rotate_data,
+// pplib.py:2406-2415), divided by 1 + 2 pi i k tau (scattering_portrait_FT,
+// pplib.py:4081-4101) when tau is given, irfft.  in == out is supported: the
+// whole row is read before the first barrier.  Dynamic LDS: nbin doubles +
+// (nbin/2 + 1) double2.
+__global__ __launch_bounds__(kBlock) void k_rotate_rows_gen(const double* in,
+                                                            const double* __restrict__ phase,
+                                                            const double* __restrict__ tau,
+                                                            double* out,
+                                                            const double2* __restrict__ tw,
+                                                            int nbin) {
+  extern __shared__ __align__(16) unsigned char gsm[];
+  double* x = reinterpret_cast<double*>(gsm);
+  double2* X = reinterpret_cast<double2*>(gsm + (((size_t)nbin * sizeof(double) + 15) & ~(size_t)15));
+  const int r = blockIdx.x, NH = nbin / 2 + 1;
+  load_real_row(x, in + (size_t)r * nbin, nbin);
+  __syncthreads();
+  const double ph = phase ? phase[r] : 0.0;
+  const double t2 = tau ? 2.0 * M_PI * tau[r] : 0.0;
+  for (int k = threadIdx.x; k < NH; k += kBlock) {
+    double2 v = dft_bin(x, nbin, k, tw);
+    if (phase) v = cmul(v, turn_phasor((double)k, ph));
+    if (t2 != 0.0) {
+      const double w = t2 * (double)k, d = 1.0 / fma(w, w, 1.0);
+      v = cmk(fma(v.y, w, v.x) * d, fma(-v.x, w, v.y) * d);
+    }
+    X[k] = v;
+  }
+  __syncthreads();
+  for (int m = threadIdx.x; m < nbin; m += kBlock)
+    out[(size_t)r * nbin + m] = idft_sample(X, nbin, m, tw);
+}
+
+}  // namespace ppf

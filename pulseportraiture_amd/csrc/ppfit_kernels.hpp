@@ -762,7 +762,13 @@ __global__ void k_rot_accum_spec(const double2* spec, const double* phase, const
                                  int NHP);
 __global__ void k_accum_reduce(const double2* partial, double2* accum, int nsplit, size_t count);
 template <int LOGN> __global__ void k_resid_chi2(ResidArgs a, const double2* tw);
-__global__ void k_vpow(double2* vp, int N, int rows);
+__global__ void k_vpow(double2* vp, int nbin, int rows);
+// any nbin (ppfit_generic.hip)
+__global__ void k_model_spec_gen(const double* model, double2* M, double* pn, int NHP, int zero_dc,
+                                 const double2* tw, double* M2, int nbin);
+__global__ void k_data_xspec_gen(SpecArgs a, int nbin);
+__global__ void k_rotate_rows_gen(const double* in, const double* phase, const double* tau,
+                                  double* out, const double2* tw, int nbin);
 __global__ void k_gauss_port(GaussArgs g, const double* freqs, double* out);
 template <typename T>
 __global__ void k_unpack(const T* raw, const double* scl, const double* offs, int nsub, int npol,

@@ -5,4 +5,5 @@
 #include "ppfit_tnc.hip"
 #include "ppfit_ncg.hip"
 #include "ppfit_models.hip"
+#include "ppfit_generic.hip"
 #include "ppfit_capi.hip"

@@ -72,7 +72,7 @@ __device__ __forceinline__ void rs_swap(const double* v, double* out) {
 // moments (kernels.hpp), Re T_m for even m and Im T_m for odd m, and nothing
 // else -- two MFMAs per step.  Lane l supplies harmonic 4 s + (l >> 4) of
 // channel l & 15 to B and v^(2 (l & 15)), v^(2 (l & 15) + 1) of that harmonic
-// to A (v is exact since N is a power of two).  X rows stream through
+// to A (v is exact when N is a power of two).  X rows stream through
 // registers U steps ahead of the MFMAs.  All kMT moments are kept (cnt =
 // kMT): the truncation bound then holds for any spectrum.
 // ---------------------------------------------------------------------------
@@ -120,11 +120,13 @@ __device__ __forceinline__ double2 vpow_inline(int k, double iN, int col) {
 // (k_vpow): the powers are the same for every channel, so forming them per
 // step (3 squarings and up to 5 selected products each, on every lane) would
 // cost more vector issue than the two MFMAs they feed.
-__global__ void k_vpow(double2* vp, int N, int rows) {
+// v = k / (nbin / 2): 2 / nbin is 1 / N to the bit for even nbin, and keeps
+// v y = 2 pi k d for odd nbin (taylor_cells' y = 2 pi (nbin / 2) d)
+__global__ void k_vpow(double2* vp, int nbin, int rows) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= rows * 16) return;
   const int k = i >> 4, col = i & 15;
-  vp[i] = vpow_inline(k, 1.0 / (double)N, col);
+  vp[i] = vpow_inline(k, 2.0 / (double)nbin, col);
 }
 
 // One 16-channel tile by one wave: lane l handles channel n (column l & 15 of
@@ -254,7 +256,7 @@ __device__ __forceinline__ void moment_tile8(const FitArgs& a, int c, int slot, 
     else return (on && k <= N) ? Xr[k] : cmk(0.0, 0.0);
   };
   const double2 s8 = turn_phasor(8.0, phic);
-  const double iN = 1.0 / (double)N;
+  const double iN = 2.0 / (double)a.nbin;  // as k_vpow's
   f64x4 d0 = {0.0, 0.0, 0.0, 0.0}, d1 = d0, d2 = d0, d3 = d0;
   double2 xb[UP];
 #pragma unroll

@@ -114,8 +114,10 @@ def gen_gaussian_profile(params, nbin):
         loc, wid, amp = params[2 + ig * 3:5 + ig * 3]
         model += amp * gaussian_profile(nbin, loc, wid)
     if params[1] != 0.0:
+        # n=nbin: the reference's irfft (pplib.py:850) drops a bin at odd
+        # nbin; the same for even nbin
         model = np.fft.irfft(scattering_profile_FT(float(params[1]) / nbin, nbin)
-                             * np.fft.rfft(model))
+                             * np.fft.rfft(model), n=nbin)
     return model
 
 
@@ -154,8 +156,10 @@ def gen_gaussian_portrait(model_code, params, scattering_index, phases, freqs, n
     port = np.array([gen_gaussian_profile(gp[i], nbin) for i in range(nchan)])
     if tau != 0.0:
         taus = scattering_times(float(tau) / nbin, scattering_index, freqs, nu_ref)
+        # n=nbin as the device's k_rotate_rows_gen (pplib.py:921 has no n=
+        # and returns nbin - 1 bins at odd nbin); the same for even nbin
         port = np.fft.irfft(scattering_portrait_FT(taus, nbin) *
-                            np.fft.rfft(port, axis=-1), axis=-1)
+                            np.fft.rfft(port, axis=-1), n=nbin, axis=-1)
     return port
 
 

@@ -56,14 +56,15 @@ def noise_block(nsub, nchan, nbin, sigma, seed, sub0=0):
     """sigma * N(0,1) for subints sub0 .. sub0+nsub-1 (device layout)."""
     s = np.arange(nsub, dtype=np.uint64)[:, None, None] + np.uint64(sub0)
     n = np.arange(nchan, dtype=np.uint64)[None, :, None]
-    j = np.arange(nbin // 2, dtype=np.uint64)[None, None, :]
-    shape = (nsub, nchan, nbin // 2)
+    nh = (nbin + 1) // 2  # odd nbin: the last pair's second value unused
+    j = np.arange(nh, dtype=np.uint64)[None, None, :]
+    shape = (nsub, nchan, nh)
     z0, z1 = philox_normal2(np.broadcast_to(j, shape), np.broadcast_to(n, shape),
                             np.broadcast_to(s & np.uint64(_MASK), shape),
                             np.broadcast_to(s >> np.uint64(32), shape), seed)
     out = np.empty((nsub, nchan, nbin))
     out[..., 0::2] = z0
-    out[..., 1::2] = z1
+    out[..., 1::2] = z1[..., :nbin // 2]
     return sigma * out
 
 
