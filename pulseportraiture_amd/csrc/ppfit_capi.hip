@@ -1011,7 +1011,7 @@ int ppf_phase_shift_batch(ppf_ctx* ctx, int32_t nprof, int32_t nbin, const doubl
   if (nprof <= 0) return PPF_OK;
   if (Ns < 2) return fail(ctx, PPF_ERR_INVALID, "Ns must be >= 2");
   int logN;
-  if (int r = check_nbin(ctx, nbin, &logN)) return r;
+  if (int r = check_nbin_any(ctx, nbin, &logN)) return r;
   HIPCHK(ctx, hipSetDevice(ctx->device));
   // number of template rows = 1 + max(model_idx); the caller sizes model.
   int nmodel = 1;
@@ -1043,6 +1043,9 @@ int ppf_phase_shift_batch(ppf_ctx* ctx, int32_t nprof, int32_t nbin, const doubl
   pa.out = out;
   pa.tw = tw;
   return timed(ctx, PPF_K_PHASE_SHIFT, [&] {
+    if (logN < 0)
+      hipLaunchKernelGGL(k_phase_shift_gen, dim3(nprof), dim3(kBlock), gen_rot_lds(nbin),
+                         ctx->stream, pa, nbin);
     LOGN_SWITCH(logN, hipLaunchKernelGGL(k_phase_shift<LG>, dim3(nprof), dim3(kBlock), 0,
                                          ctx->stream, pa));
   });
@@ -1231,12 +1234,15 @@ int ppf_irfft_rows(ppf_ctx* ctx, int32_t nrow, int32_t nbin, const double* spec,
   if (!ctx || !spec || !out) return fail(ctx, PPF_ERR_INVALID, "null argument");
   if (nrow <= 0) return PPF_OK;
   int logN;
-  if (int r = check_nbin(ctx, nbin, &logN)) return r;
+  if (int r = check_nbin_any(ctx, nbin, &logN)) return r;
   HIPCHK(ctx, hipSetDevice(ctx->device));
   const double2* tw;
   if (int r = twiddles(ctx, nbin, &tw)) return r;
   const double2* sp = reinterpret_cast<const double2*>(spec);
   return timed(ctx, PPF_K_IRFFT, [&] {
+    if (logN < 0)
+      hipLaunchKernelGGL(k_irfft_rows_gen, dim3(nrow), dim3(kBlock),
+                         (size_t)(nbin / 2 + 1) * sizeof(double2), ctx->stream, sp, out, tw, nbin);
     LOGN_SWITCH(logN, hipLaunchKernelGGL(k_irfft_rows<LG>, dim3(nrow), dim3(kBlock), 0,
                                          ctx->stream, sp, out, tw));
   });
@@ -1246,12 +1252,15 @@ int ppf_noise_rows(ppf_ctx* ctx, int32_t nrow, int32_t nbin, const double* in, d
   if (!ctx || !in || !out) return fail(ctx, PPF_ERR_INVALID, "null argument");
   if (nrow <= 0) return PPF_OK;
   int logN;
-  if (int r = check_nbin(ctx, nbin, &logN)) return r;
+  if (int r = check_nbin_any(ctx, nbin, &logN)) return r;
   HIPCHK(ctx, hipSetDevice(ctx->device));
   const double2* tw;
   if (int r = twiddles(ctx, nbin, &tw)) return r;
   const int kc = noise_kc(nbin);
   return timed(ctx, PPF_K_NOISE, [&] {
+    if (logN < 0)
+      hipLaunchKernelGGL(k_noise_rows_gen, dim3(nrow), dim3(kBlock), gen_row_lds(nbin),
+                         ctx->stream, in, out, kc, tw, nbin);
     LOGN_SWITCH(logN, hipLaunchKernelGGL(k_noise_rows<LG>, dim3(nrow), dim3(kBlock), 0,
                                          ctx->stream, in, out, kc, tw));
   });
@@ -1287,7 +1296,7 @@ int ppf_rotate_accumulate(ppf_ctx* ctx, int32_t nsub, int32_t nchan, int32_t nbi
     return fail(ctx, PPF_ERR_INVALID, "null argument");
   if (nsub <= 0 || nchan <= 0) return PPF_OK;
   int logN;
-  if (int r = check_nbin(ctx, nbin, &logN)) return r;
+  if (int r = check_nbin_any(ctx, nbin, &logN)) return r;
   HIPCHK(ctx, hipSetDevice(ctx->device));
   const double2* tw;
   if (int r = twiddles(ctx, nbin, &tw)) return r;
@@ -1304,7 +1313,11 @@ int ppf_rotate_accumulate(ppf_ctx* ctx, int32_t nsub, int32_t nchan, int32_t nbi
   if (int r = ensure(ctx, ctx->aux, (size_t)nsplit * count * sizeof(double2))) return r;
   double2* partial = reinterpret_cast<double2*>(ctx->aux.p);
   if (int r = timed(ctx, PPF_K_ROT_ACCUM, [&] {
-        if (wave)
+        if (logN < 0)
+          hipLaunchKernelGGL(k_rot_accum_gen, dim3(nsplit * nchan), dim3(kBlock),
+                             gen_row_lds(nbin), ctx->stream, data, phase, weight, partial, nsub,
+                             nchan, nsplit, tw, nbin);
+        else if (wave)
           hipLaunchKernelGGL(k_rot_accum_w, dim3(nsplit * nchan), dim3(256), 0,
                              ctx->stream, data, phase, weight, partial, nsub, nchan, nsplit, tw);
         else
@@ -1482,12 +1495,15 @@ int ppf_resid_chi2_rows(ppf_ctx* ctx, int32_t nrow, int32_t nbin, const double* 
   if (nrow <= 0) return PPF_OK;
   if (!(dof > 0.0)) return fail(ctx, PPF_ERR_INVALID, "dof must be > 0");
   int logN;
-  if (int r = check_nbin(ctx, nbin, &logN)) return r;
+  if (int r = check_nbin_any(ctx, nbin, &logN)) return r;
   HIPCHK(ctx, hipSetDevice(ctx->device));
   const double2* tw;
   if (int r = twiddles(ctx, nbin, &tw)) return r;
   ResidArgs ra{data, phase, model, model_row, scale, tau, errs, dof, out};
   return timed(ctx, PPF_K_RESID, [&] {
+    if (logN < 0)
+      hipLaunchKernelGGL(k_resid_chi2_gen, dim3(nrow), dim3(kBlock), gen_rot_lds(nbin),
+                         ctx->stream, ra, tw, nbin);
     LOGN_SWITCH(logN, hipLaunchKernelGGL(k_resid_chi2<LG>, dim3(nrow), dim3(kBlock), 0,
                                          ctx->stream, ra, tw));
   });

@@ -4,9 +4,9 @@
 // length the archive has (pptoaslib.py:976-978, pplib.py:2338-2426).  The
 // register and LDS FFTs of ppfit_spectra.hip are built per power of two; for
 // every other nbin in [64, 8192] these kernels take their place in the fit
-// entry point, the template spectra and the row rotations: the same outputs
-// (the spectra's layout, X, sig, dsum, R, rotated rows) from direct sums,
-// O(nbin^2) per row instead of O(nbin log nbin).
+// entry point, the template spectra, the row rotations, FFTFIT, the noise
+// rows, irfft, the zapping residuals and ppalign's rotate-and-sum: the same
+// outputs from direct sums, O(nbin^2) per row instead of O(nbin log nbin).
 //
 // Bin k of a real row: D_k = sum_m x_m e^{-2 pi i m k / nbin}.  The phasor
 // advances by one complex product per term and is re-seeded from the twiddle
@@ -223,6 +223,182 @@ __global__ __launch_bounds__(kBlock) void k_rotate_rows_gen(const double* in,
   __syncthreads();
   for (int m = threadIdx.x; m < nbin; m += kBlock)
     out[(size_t)r * nbin + m] = idft_sample(X, nbin, m, tw);
+}
+
+// LDS layout of the kernels below: a real row (nbin doubles, 16-B aligned
+// end) followed by one spectrum (nbin/2 + 1 double2)
+__device__ __forceinline__ double2* gen_spec_after_row(unsigned char* sm, int nbin) {
+  return reinterpret_cast<double2*>(sm + (((size_t)nbin * sizeof(double) + 15) & ~(size_t)15));
+}
+
+// k_phase_shift for any nbin: fit_phase_shift (pplib.py:2054-2100) on each
+// profile -- spectrum, noise, then the shared brute-force + Nelder-Mead
+// search (guess_search) on rm_k = D_k conj(M_k).
+__global__ __launch_bounds__(kBlock) void k_phase_shift_gen(PhaseShiftArgs a, int nbin) {
+  extern __shared__ __align__(16) unsigned char gsm[];
+  double* x = reinterpret_cast<double*>(gsm);
+  double2* rm = gen_spec_after_row(gsm, nbin);
+  __shared__ GuessShared gs;
+  const int r = blockIdx.x, tid = threadIdx.x, NH = nbin / 2 + 1;
+  load_real_row(x, a.data + (size_t)r * nbin, nbin);
+  __syncthreads();
+  const int midx = a.model_idx ? a.model_idx[r] : 0;
+  const double2* Mr = a.M + (size_t)midx * a.NHP;
+  double pnoise = 0.0, dd = 0.0, pp = 0.0;
+  for (int k = tid; k < NH; k += kBlock) {
+    double2 v = dft_bin(x, nbin, k, a.tw);
+    if (k >= a.kc) pnoise += cabs2(v);
+    if (k == 0) v = cmk(0.0, 0.0);
+    dd += cabs2(v);
+    pp += cabs2(Mr[k]);
+    rm[k] = cmulc(v, Mr[k]);
+  }
+  pnoise = block_sum(pnoise, gs.red);
+  dd = block_sum(dd, gs.red);
+  pp = block_sum(pp, gs.red);
+  double noise = a.noise ? a.noise[r] : NAN;
+  if (isnan(noise)) noise = sqrt(pnoise / (double)nbin / (double)(NH - a.kc));
+  const double err = noise * sqrt(0.5 * (double)nbin);
+  const double ie2 = 1.0 / (err * err);
+  guess_search(rm, NH, ie2, a.Ns, a.lo, a.hi, gs);
+  if (tid == 0) {
+    const double fmin = gs.fx;
+    gs.out[0] = gs.x;
+    gs.out[1] = -fmin / (pp * ie2);
+    gs.out[2] = dd * ie2;
+    gs.out[3] = pp * ie2;
+    gs.out[4] = fmin;
+  }
+  __syncthreads();
+  double c2 = 0.0;  // second derivative at the phase (pplib.py:1270-1280)
+  for (int k = tid; k < NH; k += kBlock) {
+    const double2 w = cmul(rm[k], turn_phasor((double)k, gs.out[0]));
+    c2 += (double)k * (double)k * w.x;
+  }
+  c2 = block_sum(c2, gs.red);
+  if (tid == 0) {
+    const double d2 = 4.0 * kPi * kPi * c2 * ie2;
+    const double scale = gs.out[1], d = gs.out[2], p = gs.out[3], fmin = gs.out[4];
+    double* o = a.out + (size_t)r * 6;
+    o[0] = gs.out[0];
+    o[1] = pow(scale * d2, -0.5);
+    o[2] = scale;
+    o[3] = pow(p, -0.5);
+    o[4] = pow(scale * scale * p, 0.5);
+    o[5] = (d - fmin * fmin / p) / (double)(nbin - 2);
+  }
+}
+
+// spec[r][k] = rfft(in[r])[k], k <= nbin/2 (numpy layout)
+__global__ __launch_bounds__(kBlock) void k_rfft_rows_gen(const double* __restrict__ in,
+                                                          double2* __restrict__ spec,
+                                                          const double2* __restrict__ tw, int nbin) {
+  extern __shared__ __align__(16) unsigned char gsm[];
+  double* x = reinterpret_cast<double*>(gsm);
+  const int r = blockIdx.x, NH = nbin / 2 + 1;
+  load_real_row(x, in + (size_t)r * nbin, nbin);
+  __syncthreads();
+  for (int k = threadIdx.x; k < NH; k += kBlock) spec[(size_t)r * NH + k] = dft_bin(x, nbin, k, tw);
+}
+
+// out[r] = irfft(spec[r], n = nbin)
+__global__ __launch_bounds__(kBlock) void k_irfft_rows_gen(const double2* __restrict__ spec,
+                                                           double* __restrict__ out,
+                                                           const double2* __restrict__ tw,
+                                                           int nbin) {
+  extern __shared__ __align__(16) unsigned char gsm[];
+  double2* X = reinterpret_cast<double2*>(gsm);
+  const int r = blockIdx.x, NH = nbin / 2 + 1;
+  for (int k = threadIdx.x; k < NH; k += kBlock) X[k] = spec[(size_t)r * NH + k];
+  __syncthreads();
+  for (int m = threadIdx.x; m < nbin; m += kBlock)
+    out[(size_t)r * nbin + m] = idft_sample(X, nbin, m, tw);
+}
+
+// get_noise_PS per row (pplib.py:2227-2253)
+__global__ __launch_bounds__(kBlock) void k_noise_rows_gen(const double* __restrict__ in,
+                                                           double* __restrict__ out, int kc,
+                                                           const double2* __restrict__ tw,
+                                                           int nbin) {
+  extern __shared__ __align__(16) unsigned char gsm[];
+  double* x = reinterpret_cast<double*>(gsm);
+  __shared__ double red[kWaves];
+  const int r = blockIdx.x, NH = nbin / 2 + 1;
+  load_real_row(x, in + (size_t)r * nbin, nbin);
+  __syncthreads();
+  double p = 0.0;
+  for (int k = kc + threadIdx.x; k < NH; k += kBlock) p += cabs2(dft_bin(x, nbin, k, tw));
+  p = block_sum(p, red);
+  if (threadIdx.x == 0) out[r] = sqrt(p / (double)nbin / (double)(NH - kc));
+}
+
+// ppalign's weighted rotate-and-sum (ppalign.py:202-208) for any nbin:
+// partial[p][n][k] = sum_{s in slice p} w[s][n] rfft(data[s][n])_k e^{2 pi i k ph[s][n]},
+// each k summed by one thread in subint order.
+__global__ __launch_bounds__(kBlock) void k_rot_accum_gen(const double* __restrict__ data,
+                                                          const double* __restrict__ phase,
+                                                          const double* __restrict__ weight,
+                                                          double2* __restrict__ partial, int nsub,
+                                                          int nchan, int nsplit,
+                                                          const double2* __restrict__ tw,
+                                                          int nbin) {
+  extern __shared__ __align__(16) unsigned char gsm[];
+  double* x = reinterpret_cast<double*>(gsm);
+  const int n = blockIdx.x % nchan, p = blockIdx.x / nchan, NH = nbin / 2 + 1;
+  const int per = (nsub + nsplit - 1) / nsplit;
+  const int s0 = p * per, s1 = min(nsub, s0 + per);
+  double2* out = partial + ((size_t)p * nchan + n) * NH;
+  for (int k = threadIdx.x; k < NH; k += kBlock) out[k] = cmk(0.0, 0.0);
+  for (int s = s0; s < s1; ++s) {
+    const size_t row = (size_t)s * nchan + n;
+    const double w = weight[row];
+    if (w == 0.0) continue;  // uniform per block
+    __syncthreads();
+    load_real_row(x, data + row * nbin, nbin);
+    __syncthreads();
+    const double ph = phase[row];
+    for (int k = threadIdx.x; k < NH; k += kBlock)
+      out[k] = cadd(out[k], cscale(cmul(dft_bin(x, nbin, k, tw), turn_phasor((double)k, ph)), w));
+  }
+}
+
+// k_resid_chi2 for any nbin (pptoas.py:1389-1402, get_red_chi2 pplib.py:727-749):
+// Parseval on R = D e^{2 pi i k phase} - scale M / (1 + 2 pi i k tau); irfft
+// keeps only Re R_0 (and Re R_{nbin/2} for even nbin).
+__global__ __launch_bounds__(kBlock) void k_resid_chi2_gen(ResidArgs a,
+                                                           const double2* __restrict__ tw,
+                                                           int nbin) {
+  extern __shared__ __align__(16) unsigned char gsm[];
+  double* x = reinterpret_cast<double*>(gsm);
+  double2* D = gen_spec_after_row(gsm, nbin);
+  __shared__ double red[kWaves];
+  const int r = blockIdx.x, NH = nbin / 2 + 1;
+  load_real_row(x, a.data + (size_t)r * nbin, nbin);
+  __syncthreads();
+  const double ph = a.phase ? a.phase[r] : 0.0;
+  for (int k = threadIdx.x; k < NH; k += kBlock)
+    D[k] = cmul(dft_bin(x, nbin, k, tw), turn_phasor((double)k, ph));
+  __syncthreads();
+  load_real_row(x, a.model + (size_t)(a.model_row ? a.model_row[r] : r) * nbin, nbin);
+  __syncthreads();
+  const double sc = a.scale[r];
+  const double t2 = a.tau ? 2.0 * M_PI * a.tau[r] : 0.0;
+  double acc = 0.0;
+  for (int k = threadIdx.x; k < NH; k += kBlock) {
+    double2 m = dft_bin(x, nbin, k, tw);
+    if (t2 != 0.0) {
+      const double w = t2 * (double)k, d = 1.0 / fma(w, w, 1.0);
+      m = cmk(fma(m.y, w, m.x) * d, fma(-m.x, w, m.y) * d);
+    }
+    const double2 q = cmk(fma(-sc, m.x, D[k].x), fma(-sc, m.y, D[k].y));
+    const bool real_only = k == 0 || (!(nbin & 1) && k == nbin / 2);
+    acc += real_only ? q.x * q.x : 2.0 * cabs2(q);
+  }
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) {
+    const double e = a.errs[r];
+    a.out[r] = acc / (double)nbin / (e * e) / a.dof;
+  }
 }
 
 }  // namespace ppf

@@ -769,6 +769,14 @@ __global__ void k_model_spec_gen(const double* model, double2* M, double* pn, in
 __global__ void k_data_xspec_gen(SpecArgs a, int nbin);
 __global__ void k_rotate_rows_gen(const double* in, const double* phase, const double* tau,
                                   double* out, const double2* tw, int nbin);
+__global__ void k_phase_shift_gen(PhaseShiftArgs a, int nbin);
+__global__ void k_rfft_rows_gen(const double* in, double2* spec, const double2* tw, int nbin);
+__global__ void k_irfft_rows_gen(const double2* spec, double* out, const double2* tw, int nbin);
+__global__ void k_noise_rows_gen(const double* in, double* out, int kc, const double2* tw, int nbin);
+__global__ void k_rot_accum_gen(const double* data, const double* phase, const double* weight,
+                                double2* partial, int nsub, int nchan, int nsplit,
+                                const double2* tw, int nbin);
+__global__ void k_resid_chi2_gen(ResidArgs a, const double2* tw, int nbin);
 __global__ void k_gauss_port(GaussArgs g, const double* freqs, double* out);
 template <typename T>
 __global__ void k_unpack(const T* raw, const double* scl, const double* offs, int nsub, int npol,

@@ -15,7 +15,9 @@ take direct-sum kernels instead.  Checked here against the oracle (numpy):
   TNC golden tests: within 1e-3 sigma of the oracle's end point or of one of
   its own end points under a channel reordering or a one-ulp restart, and
   TNC's FCONVERGED (1) and LSFAIL (4) taken as one converged status;
-- get_TOAs end to end on an archive of 1000-bin profiles.
+- get_noise_PS, irfft, fit_phase_shift, the zapping residual chi2 and
+  ppalign's rotate-and-sum rows against numpy / the oracle;
+- get_TOAs and ppalign.align_archives end to end on 1000-bin archives.
 """
 import numpy as np
 import pytest
@@ -197,3 +199,79 @@ def test_get_toas_generic_nbin(tmp_path):
     # the synthetic truth: within a few sigma of the injected phase / DM
     dms = np.asarray(gt.DMs[0])
     assert np.all(np.abs(dms - (w.DM0 + w.dDM)) < 6 * np.asarray(gt.DM_errs[0]))
+
+
+@pytest.mark.parametrize("nbin", [1000, 999])
+def test_row_entry_points_generic(eng, nbin):
+    """get_noise_PS, irfft, fit_phase_shift (ppalign / pplib FFTFIT), the
+    zapping residual chi2 and ppalign's rotate-and-sum at a generic nbin,
+    against numpy / the oracle."""
+    import torch
+    w = synth.make_workload(1, 6, nbin, seed=730 + nbin)
+    data = synth.workload_data_host(w)[0]
+    np.testing.assert_allclose(eng.noise_rows(data).cpu().numpy(),
+                               O.get_noise_PS(data, chans=True), rtol=1e-10)
+    spec = np.fft.rfft(data, axis=-1)
+    np.testing.assert_allclose(eng.irfft_rows(spec, nbin).cpu().numpy(),
+                               np.fft.irfft(spec, n=nbin, axis=-1), rtol=0,
+                               atol=1e-12 * np.abs(data).max())
+    out = eng.phase_shift_batch(data, w.model, model_idx=np.arange(6)).cpu().numpy()
+    for i in range(6):
+        ref = O.fit_phase_shift(data[i], w.model[i])
+        d = abs(out[i, 0] - ref.phase)
+        assert min(d, 1.0 - d) <= 1e-3 * ref.phase_err, i
+        np.testing.assert_allclose(out[i, 1:], [ref.phase_err, ref.scale, ref.scale_err, ref.snr,
+                                                ref.red_chi2], rtol=1e-6)
+    k = np.arange(nbin // 2 + 1)
+    ph = np.linspace(-0.3, 0.4, 6)
+    tau = np.linspace(0.0, 2e-3, 6)
+    sc, errs = np.linspace(0.9, 1.1, 6), np.full(6, 1.5)
+    got = eng.resid_chi2_rows(data, ph, w.model, sc, errs, 100.0, tau=tau).cpu().numpy()
+    rot = np.fft.irfft(spec * np.exp(2j * np.pi * np.outer(ph, k)), n=nbin, axis=-1)
+    msc = np.fft.irfft(np.fft.rfft(w.model, axis=-1) / (1 + 2j * np.pi * np.outer(tau, k)),
+                       n=nbin, axis=-1)
+    ref = np.sum((rot - sc[:, None] * msc) ** 2, axis=-1) / errs ** 2 / 100.0
+    np.testing.assert_allclose(got, ref, rtol=1e-9)
+    d3 = np.stack([data, 0.5 * data[::-1]])  # [nsub 2, nchan 6, nbin]
+    phs = np.stack([ph, -ph])
+    wts = np.array([[1.0] * 6, [0.5, 0.0, 1.0, 2.0, 1.0, 1.0]])
+    acc = torch.zeros(6, nbin // 2 + 1, 2, dtype=torch.float64, device=eng.device)
+    eng.rotate_accumulate(d3, phs, wts, acc)
+    torch.cuda.synchronize()
+    ref = np.sum(wts[..., None] * np.fft.rfft(d3, axis=-1) *
+                 np.exp(2j * np.pi * phs[..., None] * k), axis=0)
+    got = acc.cpu().numpy()
+    np.testing.assert_allclose(got[..., 0] + 1j * got[..., 1], ref, rtol=0,
+                               atol=1e-12 * np.abs(ref).max())
+
+
+def test_align_archives_generic_nbin():
+    """ppalign.align_archives on 1000-bin archives (no data-spectrum cache at
+    this length): runs end to end, and the aligned portrait is the template
+    up to noise (every channel correlates with it)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from pulseportraiture_amd import archive, ppalign
+    from tests.golden_consts import DM0
+    nbin, nchan = 1000, 16
+    names = []
+    for i in range(3):
+        w = synth.make_workload(2, nchan, nbin, seed=740 + i, sigma=0.3)
+        archive.register_archive("gal_%d" % i, dict(
+            subints=synth.workload_data_host(w)[:, None], freqs=w.freqs, Ps=np.full(2, w.P),
+            epochs=[(57000 + i, 0, 0.0), (57000 + i, 60, 0.0)], DM=DM0, nu0=1500.0, dmc=0,
+            weights=np.ones((2, nchan))))
+        names.append("gal_%d" % i)
+    archive.register_archive("gal_guess", dict(subints=w.model[None, None], freqs=w.freqs,
+                                               Ps=[w.P], epochs=[(57000, 0, 0.0)], DM=DM0,
+                                               nu0=1500.0, dmc=1))
+    try:
+        port = np.asarray(ppalign.align_archives(names, "gal_guess", niter=2, quiet=True))
+    finally:
+        for n in names + ["gal_guess"]:
+            archive.unregister_archive(n)
+    assert port.shape[-2:] == (nchan, nbin) and np.all(np.isfinite(port))
+    p = port.reshape(-1, nchan, nbin)[0]
+    for n in range(nchan):
+        assert np.corrcoef(p[n], w.model[n])[0, 1] > 0.99, n
