@@ -1108,8 +1108,8 @@ int ppf_spline_portraits(ppf_ctx* ctx, int32_t nrow, int32_t nbin_in, int32_t nb
   int logI = 0, logO = 0;
   const bool resample = nbin_in != nbin;
   if (resample) {
-    if (int r = check_nbin(ctx, nbin_in, &logI)) return r;
-    if (int r = check_nbin(ctx, nbin, &logO)) return r;
+    if (int r = check_nbin_any(ctx, nbin_in, &logI)) return r;
+    if (int r = check_nbin_any(ctx, nbin, &logO)) return r;
   } else if (nbin <= 0) {
     return fail(ctx, PPF_ERR_INVALID, "nbin=%d", nbin);
   }
@@ -1153,10 +1153,16 @@ int ppf_spline_portraits(ppf_ctx* ctx, int32_t nrow, int32_t nbin_in, int32_t nb
   const double shift = 0.5 * (1.0 / (double)nbin - 1.0 / (double)nbin_in);
   const size_t ny = (size_t)nrow * hout;
   return timed(ctx, PPF_K_MODEL_FFT, [&] {
+    if (logI < 0)
+      hipLaunchKernelGGL(k_rfft_rows_gen, dim3(nrow), dim3(kBlock), gen_row_lds(nbin_in),
+                         ctx->stream, rows, X, twi, nbin_in);
     LOGN_SWITCH(logI, hipLaunchKernelGGL(k_rfft_rows<LG>, dim3(nrow), dim3(kBlock), 0, ctx->stream,
                                          rows, X, twi));
     hipLaunchKernelGGL(k_resample_spec, dim3((unsigned)((ny + 255) / 256)), dim3(256), 0,
                        ctx->stream, X, nbin_in, nbin, shift, nrow, Y);
+    if (logO < 0)
+      hipLaunchKernelGGL(k_irfft_rows_gen, dim3(nrow), dim3(kBlock), hout * sizeof(double2),
+                         ctx->stream, Y, out, two, nbin);
     LOGN_SWITCH(logO, hipLaunchKernelGGL(k_irfft_rows<LG>, dim3(nrow), dim3(kBlock), 0,
                                          ctx->stream, Y, out, two));
   });
@@ -1194,7 +1200,7 @@ int ppf_instrumental_response_rows(ppf_ctx* ctx, int32_t nrow, int32_t nbin, con
   g.P = P;
   if (DM != 0.0 && !(P > 0.0)) return fail(ctx, PPF_ERR_INVALID, "P=%g", P);
   int logN;
-  if (int r = check_nbin(ctx, nbin, &logN)) return r;
+  if (int r = check_nbin_any(ctx, nbin, &logN)) return r;
   HIPCHK(ctx, hipSetDevice(ctx->device));
   const size_t nh = (size_t)nbin / 2 + 1, n = (size_t)nrow * nh;
   const unsigned grid = (unsigned)((n + 255) / 256);
@@ -1208,10 +1214,16 @@ int ppf_instrumental_response_rows(ppf_ctx* ctx, int32_t nrow, int32_t nbin, con
   const double2* tw;
   if (int r = twiddles(ctx, nbin, &tw)) return r;
   return timed(ctx, PPF_K_MODEL_FFT, [&] {
+    if (logN < 0)
+      hipLaunchKernelGGL(k_rfft_rows_gen, dim3(nrow), dim3(kBlock), gen_row_lds(nbin),
+                         ctx->stream, in, X, tw, nbin);
     LOGN_SWITCH(logN, hipLaunchKernelGGL(k_rfft_rows<LG>, dim3(nrow), dim3(kBlock), 0, ctx->stream,
                                          in, X, tw));
     hipLaunchKernelGGL(k_ir_spec, dim3(grid), dim3(256), 0, ctx->stream, X, nullptr, nrow, (int)nh,
                        g, freqs);
+    if (logN < 0)
+      hipLaunchKernelGGL(k_irfft_rows_gen, dim3(nrow), dim3(kBlock), nh * sizeof(double2),
+                         ctx->stream, X, out, tw, nbin);
     LOGN_SWITCH(logN, hipLaunchKernelGGL(k_irfft_rows<LG>, dim3(nrow), dim3(kBlock), 0,
                                          ctx->stream, X, out, tw));
   });

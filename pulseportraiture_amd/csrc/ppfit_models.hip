@@ -210,11 +210,11 @@ __global__ void k_resample_spec(const double2* __restrict__ X, int nin, int nout
   const int N = min(nin, nout);
   double2 y = cmk(0.0, 0.0);
   if (k < N / 2 + 1) y = X[r * hi + k];
-  if (k == N / 2) {
+  if (!(N & 1) && k == N / 2) {  // scipy adjusts the shared Nyquist bin of an even N only
     if (nout < nin) y = cscale(y, 2.0);
     else if (nin < nout) y = cscale(y, 0.5);
   }
-  if (k == nout / 2) y.y = 0.0;
+  if (!(nout & 1) && k == nout / 2) y.y = 0.0;
   y = cscale(y, (double)nout / (double)nin);
   if (shift != 0.0) y = cmul(y, turn_phasor((double)k, shift));
   Y[i] = y;

@@ -275,3 +275,51 @@ def test_align_archives_generic_nbin():
     p = port.reshape(-1, nchan, nbin)[0]
     for n in range(nchan):
         assert np.corrcoef(p[n], w.model[n])[0, 1] > 0.99, n
+
+
+@pytest.mark.parametrize("nbin", [1000, 999])
+def test_instrumental_response_generic(eng, nbin):
+    """instrumental_response_port_FT (pptoaslib.py:145-179, the oracle's) and
+    its convolution of rows, irfft(R rfft(rows), n = nbin)."""
+    rng = np.random.default_rng(nbin)
+    rows = rng.normal(size=(6, nbin))
+    f = np.linspace(1200.0, 1800.0, 6)
+    R = O.instrumental_response_port_FT(nbin, f, 1.0, 0.002, [0.01], ["gauss"])
+    np.testing.assert_allclose(eng.response_table(nbin, f, 1.0, 0.002, [0.01], ["gauss"])
+                               .cpu().numpy(), np.real(R), rtol=0, atol=1e-14)
+    got = eng.instrumental_response_rows(rows, f, 1.0, 0.002, [0.01], ["gauss"]).cpu().numpy()
+    ref = np.fft.irfft(np.real(R) * np.fft.rfft(rows, axis=-1), n=nbin, axis=-1)
+    np.testing.assert_allclose(got, ref, rtol=0, atol=1e-12 * np.abs(ref).max())
+
+
+@pytest.mark.parametrize("nbin", [1000, 999, 3000])
+def test_spline_portrait_resampled_generic(tmp_path, nbin):
+    """gen_spline_portrait (pplib.py:932-956) resampled to a generic nbin:
+    scipy.signal.resample of the native-length portrait, then
+    rotate_portrait by 0.5 (1/nbin - 1/nbin_in) -- with irfft(n = nbin), where
+    the reference's rotate_portrait (pplib.py:2449-2461) drops a bin at odd
+    nbin."""
+    import json
+    import os
+    import torch
+    from scipy import signal as ss
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from pulseportraiture_amd import pplib
+    from tests.conftest import GOLDEN
+    z = np.load(os.path.join(GOLDEN, "templates_r3.npz"))
+    meta = json.load(open(os.path.join(GOLDEN, "templates_r3.json")))
+    path = tmp_path / "m3.spl"
+    path.write_bytes(bytes(z["spl_m3_file"]))
+    tag = meta["m3"]["cases"][0]
+    freqs = z["spl_m3_%s_freqs" % tag]
+    mean_prof = pplib.read_spline_model(str(path), quiet=True)[3]
+    nin = len(mean_prof)
+    _, native = pplib.read_spline_model(str(path), freqs, nin, quiet=True)
+    _, port = pplib.read_spline_model(str(path), freqs, nbin, quiet=True)
+    shift = 0.5 * (1.0 / nbin - 1.0 / nin)
+    rs = np.fft.rfft(ss.resample(np.asarray(native), nbin, axis=1), axis=1)
+    ref = np.fft.irfft(rs * np.exp(2j * np.pi * shift * np.arange(rs.shape[1])), n=nbin, axis=1)
+    port = np.asarray(port)
+    assert port.shape == ref.shape
+    assert np.max(np.abs(port - ref)) <= 1e-12 * np.max(np.abs(ref))
