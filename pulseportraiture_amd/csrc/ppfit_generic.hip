@@ -19,53 +19,76 @@ namespace ppf {
 
 constexpr int kSeed = 32;
 
-// D_k of x[0 .. nbin) (LDS); tw[j] = e^{-2 pi i j / nbin}, k < nbin
+// D_k of x[0 .. nbin) (LDS); tw[j] = e^{-2 pi i j / nbin}, k < nbin.  The
+// real input's symmetry halves the work: terms m and nbin - m share the
+// phasor, D_k = x_0 + sum_{1 <= m < nbin/2} [(x_m + x_{nbin-m}) cos -
+// i (x_m - x_{nbin-m}) sin](2 pi m k / nbin) + [nbin even] (-1)^k x_{nbin/2}.
 __device__ __forceinline__ double2 dft_bin(const double* x, int nbin, int k,
                                            const double2* __restrict__ tw) {
   const double2 w = tw[k];
+  const int M = (nbin - 1) / 2;  // pairs m = 1 .. M
   const int step = (int)(((long long)kSeed * k) % nbin);
-  double re = 0.0, im = 0.0;
-  int seed = 0;  // (m0 k) mod nbin
-  for (int m0 = 0; m0 < nbin; m0 += kSeed) {
+  double re = x[0], im = 0.0;
+  int seed = k;  // (m0 k) mod nbin at m0 = 1
+  for (int m0 = 1; m0 <= M; m0 += kSeed) {
     double2 e = tw[seed];
-    const int me = min(m0 + kSeed, nbin);
-    for (int m = m0; m < me; ++m) {
-      const double v = x[m];
-      re = fma(v, e.x, re);
-      im = fma(v, e.y, im);
+    const int me = min(m0 + kSeed - 1, M);
+    for (int m = m0; m <= me; ++m) {
+      const double a = x[m], b = x[nbin - m];
+      re = fma(a + b, e.x, re);
+      im = fma(a - b, e.y, im);
       e = cmul(e, w);
     }
     seed += step;
     if (seed >= nbin) seed -= nbin;
   }
+  if (!(nbin & 1)) re += (k & 1) ? -x[nbin / 2] : x[nbin / 2];
   return cmk(re, im);
 }
 
-// numpy irfft(X, n = nbin) at sample m: (Re X_0 + 2 sum_{1 <= k <= K} Re(X_k
-// e^{2 pi i m k / nbin}) + [nbin even] Re X_{nbin/2} (-1)^m) / nbin, K = (nbin - 1) / 2;
-// X[0 .. nbin/2] in LDS
-__device__ __forceinline__ double idft_sample(const double2* X, int nbin, int m,
-                                              const double2* __restrict__ tw) {
+// numpy irfft(X, n = nbin) at samples m and nbin - m (1 <= m < nbin/2):
+// with A = sum_{1 <= k <= K} Re X_k cos(2 pi m k / nbin) and B = sum Im X_k
+// sin(..), K = (nbin - 1) / 2, the two samples are (Re X_0 + 2 (A -+ B) +
+// [nbin even] (-1)^m Re X_{nbin/2}) / nbin; m = 0 (and m = nbin/2) alone,
+// with B = 0.  X[0 .. nbin/2] in LDS.
+__device__ __forceinline__ void idft_pair(const double2* X, int nbin, int m,
+                                          const double2* __restrict__ tw, double& out_m,
+                                          double& out_nm) {
   const double2 w = cconj(tw[m]);  // e^{+2 pi i m / nbin}
   const int K = (nbin - 1) / 2;
   const int step = (int)(((long long)kSeed * m) % nbin);
-  double acc = 0.0;
+  double A = 0.0, B = 0.0;
   int seed = m;  // (k0 m) mod nbin at k0 = 1
   for (int k0 = 1; k0 <= K; k0 += kSeed) {
     double2 e = cconj(tw[seed]);
     const int ke = min(k0 + kSeed - 1, K);
     for (int k = k0; k <= ke; ++k) {
       const double2 x = X[k];
-      acc = fma(x.x, e.x, acc);
-      acc = fma(-x.y, e.y, acc);
+      A = fma(x.x, e.x, A);
+      B = fma(x.y, e.y, B);
       e = cmul(e, w);
     }
     seed += step;
     if (seed >= nbin) seed -= nbin;
   }
-  double v = fma(2.0, acc, X[0].x);
-  if (!(nbin & 1)) v += (m & 1) ? -X[nbin / 2].x : X[nbin / 2].x;
-  return v / (double)nbin;
+  double ny = 0.0;
+  if (!(nbin & 1)) ny = (m & 1) ? -X[nbin / 2].x : X[nbin / 2].x;
+  const double inv = 1.0 / (double)nbin;
+  out_m = (fma(2.0, A - B, X[0].x) + ny) * inv;
+  out_nm = (fma(2.0, A + B, X[0].x) + ny) * inv;
+}
+
+// every sample of irfft(X, n = nbin) into out[0 .. nbin), the block's threads
+// taking the pairs (m, nbin - m)
+__device__ __forceinline__ void idft_row(const double2* X, int nbin, const double2* __restrict__ tw,
+                                         double* __restrict__ out) {
+  const int half = nbin / 2;
+  for (int m = threadIdx.x; m <= half; m += blockDim.x) {
+    double a, b;
+    idft_pair(X, nbin, m, tw, a, b);
+    out[m] = a;
+    if (m > 0 && nbin - m != m) out[nbin - m] = b;
+  }
 }
 
 __device__ __forceinline__ void load_real_row(double* x, const double* __restrict__ row, int nbin) {
@@ -221,8 +244,7 @@ __global__ __launch_bounds__(kBlock) void k_rotate_rows_gen(const double* in,
     X[k] = v;
   }
   __syncthreads();
-  for (int m = threadIdx.x; m < nbin; m += kBlock)
-    out[(size_t)r * nbin + m] = idft_sample(X, nbin, m, tw);
+  idft_row(X, nbin, tw, out + (size_t)r * nbin);
 }
 
 // LDS layout of the kernels below: a real row (nbin doubles, 16-B aligned
@@ -311,8 +333,7 @@ __global__ __launch_bounds__(kBlock) void k_irfft_rows_gen(const double2* __rest
   const int r = blockIdx.x, NH = nbin / 2 + 1;
   for (int k = threadIdx.x; k < NH; k += kBlock) X[k] = spec[(size_t)r * NH + k];
   __syncthreads();
-  for (int m = threadIdx.x; m < nbin; m += kBlock)
-    out[(size_t)r * nbin + m] = idft_sample(X, nbin, m, tw);
+  idft_row(X, nbin, tw, out + (size_t)r * nbin);
 }
 
 // get_noise_PS per row (pplib.py:2227-2253)
