@@ -46,6 +46,59 @@ __device__ __forceinline__ double2 dft_bin(const double* x, int nbin, int k,
   return cmk(re, im);
 }
 
+// Two bins at once (k1, k2 < nbin): the same sums as dft_bin for each, the
+// loads and pair sums shared and the two phasor chains interleaved.
+__device__ __forceinline__ void dft_bin2(const double* x, int nbin, int k1, int k2,
+                                         const double2* __restrict__ tw, double2& d1,
+                                         double2& d2) {
+  const double2 w1 = tw[k1], w2 = tw[k2];
+  const int M = (nbin - 1) / 2;
+  const int step1 = (int)(((long long)kSeed * k1) % nbin);
+  const int step2 = (int)(((long long)kSeed * k2) % nbin);
+  double re1 = x[0], im1 = 0.0, re2 = x[0], im2 = 0.0;
+  int seed1 = k1, seed2 = k2;
+  for (int m0 = 1; m0 <= M; m0 += kSeed) {
+    double2 e1 = tw[seed1], e2 = tw[seed2];
+    const int me = min(m0 + kSeed - 1, M);
+    for (int m = m0; m <= me; ++m) {
+      const double a = x[m], b = x[nbin - m];
+      const double sp = a + b, sm = a - b;
+      re1 = fma(sp, e1.x, re1);
+      im1 = fma(sm, e1.y, im1);
+      re2 = fma(sp, e2.x, re2);
+      im2 = fma(sm, e2.y, im2);
+      e1 = cmul(e1, w1);
+      e2 = cmul(e2, w2);
+    }
+    seed1 += step1;
+    if (seed1 >= nbin) seed1 -= nbin;
+    seed2 += step2;
+    if (seed2 >= nbin) seed2 -= nbin;
+  }
+  if (!(nbin & 1)) {
+    const double xn = x[nbin / 2];
+    re1 += (k1 & 1) ? -xn : xn;
+    re2 += (k2 & 1) ? -xn : xn;
+  }
+  d1 = cmk(re1, im1);
+  d2 = cmk(re2, im2);
+}
+
+// f(k, D_k) for every bin k < kend of the row, each thread taking k = tid +
+// blockDim q in increasing q (the order of the one-bin loop), two at a time
+template <typename F>
+__device__ __forceinline__ void dft_each_bin(const double* x, int nbin, int kend,
+                                             const double2* __restrict__ tw, F&& f) {
+  const int nt = blockDim.x;
+  for (int k = threadIdx.x; k < kend; k += 2 * nt) {
+    const int k2 = k + nt;
+    double2 d1, d2;
+    dft_bin2(x, nbin, k, k2 < kend ? k2 : k, tw, d1, d2);
+    f(k, d1);
+    if (k2 < kend) f(k2, d2);
+  }
+}
+
 // numpy irfft(X, n = nbin) at samples m and nbin - m (1 <= m < nbin/2):
 // with A = sum_{1 <= k <= K} Re X_k cos(2 pi m k / nbin) and B = sum Im X_k
 // sin(..), K = (nbin - 1) / 2, the two samples are (Re X_0 + 2 (A -+ B) +
@@ -180,18 +233,14 @@ __global__ __launch_bounds__(kBlock) void k_data_xspec_gen(SpecArgs a, int nbin)
     const double phi = Dfac * (1.0 / (fr[n] * fr[n]) - nug2);
     const double wq = a.weights ? a.weights[(size_t)s * nchan + n] : 1.0;
     double pn = 0.0, pd = 0.0;
-    for (int k = tid; k < a.NHP; k += kBlock) {
-      double2 xk = cmk(0.0, 0.0);
-      if (k < NH) {
-        const double2 d = dft_bin(x, nbin, k, a.tw);
-        const double p2 = cabs2(d);
-        if (k >= a.kc) pn += p2;
-        if (k >= 1) pd += p2;
-        if (k >= 1) xk = cmulc(d, Mr[k]);
-        if (a.guess) Rr[k] = cadd(Rr[k], cmul(d, cscale(turn_phasor((double)k, phi), wq)));
-      }
-      Xr[k] = xk;
-    }
+    dft_each_bin(x, nbin, NH, a.tw, [&](int k, double2 d) {
+      const double p2 = cabs2(d);
+      if (k >= a.kc) pn += p2;
+      if (k >= 1) pd += p2;
+      Xr[k] = k >= 1 ? cmulc(d, Mr[k]) : cmk(0.0, 0.0);
+      if (a.guess) Rr[k] = cadd(Rr[k], cmul(d, cscale(turn_phasor((double)k, phi), wq)));
+    });
+    for (int k = NH + tid; k < a.NHP; k += kBlock) Xr[k] = cmk(0.0, 0.0);
     pn = block_sum(pn, red);
     pd = block_sum(pd, red);
     if (tid == 0) {
