@@ -121,6 +121,21 @@ size_t gen_rot_lds(int nbin) {
   return (((size_t)nbin * sizeof(double) + 15) & ~(size_t)15) + (size_t)(nbin / 2 + 1) * sizeof(double2);
 }
 
+// the generic-length data pass of n subints: every row's rfft on the matrix
+// cores into the X rows, then the per-subint pass (ppfit_generic.hip)
+void launch_data_gen(const SpecArgs& sa, int n, int nbin, hipStream_t st) {
+  const int nrows = n * sa.nchan, NH = nbin / 2 + 1;
+  const double* rows = sa.data + (size_t)sa.sub0 * sa.nchan * nbin;
+  const dim3 g((nrows + 15) / 16, (NH + 255) / 256);
+  if (nbin <= kGenLdsTw)
+    hipLaunchKernelGGL(k_dft_rows_mfma<true>, g, dim3(kBlock), dft_mfma_lds(nbin, true), st,
+                       rows, sa.X, nrows, nbin, sa.NHP, sa.tw);
+  else
+    hipLaunchKernelGGL(k_dft_rows_mfma<false>, g, dim3(kBlock), dft_mfma_lds(nbin, false), st,
+                       rows, sa.X, nrows, nbin, sa.NHP, sa.tw);
+  hipLaunchKernelGGL(k_data_post_gen, dim3(n), dim3(kBlock), 0, st, sa, nbin);
+}
+
 // the table of nbin in a generic-length cache (created by make on first use)
 template <typename F>
 int gen_table(ppf_ctx* ctx, std::vector<std::pair<int, double2*>>& cache, int nbin, size_t n,
@@ -745,9 +760,7 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
         bind_spec(sp, fp, s0 + off);
         if (prev_x) HIPCHK(ctx, hipStreamWaitEvent(st, prev_x, 0));
         if (int r = timed_on(ctx, PPF_K_DATA_XSPEC, st, [&] {
-              if (logN < 0)
-                hipLaunchKernelGGL(k_data_xspec_gen, dim3(n), dim3(kBlock), gen_row_lds(nbin), st,
-                                   sp, nbin);
+              if (logN < 0) launch_data_gen(sp, n, nbin, st);
               LOGN_SWITCH(logN, WIDE_SWITCH(wide, hipLaunchKernelGGL((k_data_xspec<LG, WD>), dim3(n),
                                                    dim3(XspecCfg<LG>::WPB * 64),
                                                    lds_xspec, st, sp)));
@@ -805,9 +818,7 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
     fa.sub0 = (int)s0;
     bind_spec(sa, fa, s0);
     if (int r = timed(ctx, PPF_K_DATA_XSPEC, [&] {
-          if (logN < 0)
-            hipLaunchKernelGGL(k_data_xspec_gen, dim3(nc), dim3(kBlock), gen_row_lds(nbin),
-                               ctx->stream, sa, nbin);
+          if (logN < 0) launch_data_gen(sa, nc, nbin, ctx->stream);
           LOGN_SWITCH(logN, WIDE_SWITCH(wide, hipLaunchKernelGGL((k_data_xspec<LG, WD>), dim3(nc),
                                                                  dim3(XspecCfg<LG>::WPB * 64),
                                                                  lds_xspec, ctx->stream, sa)));

@@ -8,11 +8,13 @@
 // rows, irfft, the zapping residuals and ppalign's rotate-and-sum: the same
 // outputs from direct sums, O(nbin^2) per row instead of O(nbin log nbin).
 //
-// Bin k of a real row: D_k = sum_m x_m e^{-2 pi i m k / nbin}.  The phasor
-// advances by one complex product per term and is re-seeded from the twiddle
-// table at the exact index (m k) mod nbin every kSeed terms, so its rounding
-// never grows past kSeed products (relative error ~1e-15, against the
-// north_star tolerance of 1e-3 sigma on the fitted parameters).
+// Bin k of a real row: D_k = sum_m x_m e^{-2 pi i m k / nbin}.  The fit's
+// data pass forms all of them as a GEMM on the fp64 matrix cores against
+// the twiddle table (k_dft_rows_mfma); the other row kernels sum one bin per
+// thread, the phasor advancing by one complex product per term and re-seeded
+// from the table at the exact index (m k) mod nbin every kSeed terms, so its
+// rounding never grows past kSeed products (relative error ~1e-15, against
+// the north_star tolerance of 1e-3 sigma on the fitted parameters).
 #include "ppfit_kernels.hpp"
 
 namespace ppf {
@@ -44,59 +46,6 @@ __device__ __forceinline__ double2 dft_bin(const double* x, int nbin, int k,
   }
   if (!(nbin & 1)) re += (k & 1) ? -x[nbin / 2] : x[nbin / 2];
   return cmk(re, im);
-}
-
-// Two bins at once (k1, k2 < nbin): the same sums as dft_bin for each, the
-// loads and pair sums shared and the two phasor chains interleaved.
-__device__ __forceinline__ void dft_bin2(const double* x, int nbin, int k1, int k2,
-                                         const double2* __restrict__ tw, double2& d1,
-                                         double2& d2) {
-  const double2 w1 = tw[k1], w2 = tw[k2];
-  const int M = (nbin - 1) / 2;
-  const int step1 = (int)(((long long)kSeed * k1) % nbin);
-  const int step2 = (int)(((long long)kSeed * k2) % nbin);
-  double re1 = x[0], im1 = 0.0, re2 = x[0], im2 = 0.0;
-  int seed1 = k1, seed2 = k2;
-  for (int m0 = 1; m0 <= M; m0 += kSeed) {
-    double2 e1 = tw[seed1], e2 = tw[seed2];
-    const int me = min(m0 + kSeed - 1, M);
-    for (int m = m0; m <= me; ++m) {
-      const double a = x[m], b = x[nbin - m];
-      const double sp = a + b, sm = a - b;
-      re1 = fma(sp, e1.x, re1);
-      im1 = fma(sm, e1.y, im1);
-      re2 = fma(sp, e2.x, re2);
-      im2 = fma(sm, e2.y, im2);
-      e1 = cmul(e1, w1);
-      e2 = cmul(e2, w2);
-    }
-    seed1 += step1;
-    if (seed1 >= nbin) seed1 -= nbin;
-    seed2 += step2;
-    if (seed2 >= nbin) seed2 -= nbin;
-  }
-  if (!(nbin & 1)) {
-    const double xn = x[nbin / 2];
-    re1 += (k1 & 1) ? -xn : xn;
-    re2 += (k2 & 1) ? -xn : xn;
-  }
-  d1 = cmk(re1, im1);
-  d2 = cmk(re2, im2);
-}
-
-// f(k, D_k) for every bin k < kend of the row, each thread taking k = tid +
-// blockDim q in increasing q (the order of the one-bin loop), two at a time
-template <typename F>
-__device__ __forceinline__ void dft_each_bin(const double* x, int nbin, int kend,
-                                             const double2* __restrict__ tw, F&& f) {
-  const int nt = blockDim.x;
-  for (int k = threadIdx.x; k < kend; k += 2 * nt) {
-    const int k2 = k + nt;
-    double2 d1, d2;
-    dft_bin2(x, nbin, k, k2 < kend ? k2 : k, tw, d1, d2);
-    f(k, d1);
-    if (k2 < kend) f(k2, d2);
-  }
 }
 
 // numpy irfft(X, n = nbin) at samples m and nbin - m (1 <= m < nbin/2):
@@ -175,93 +124,6 @@ __global__ __launch_bounds__(kBlock) void k_model_spec_gen(const double* __restr
   }
   p = block_sum(p, red);
   if (threadIdx.x == 0 && pn) pn[row] = p;
-}
-
-// k_data_xspec for any nbin: one workgroup per subint, its channel rows in
-// order.  Per fitted channel: D = rfft(row); sig = errs or get_noise_PS
-// (pplib.py:2227-2253); dsum = sum_{k>=1} |D_k|^2; X_k = D_k conj(M_k) (0 at
-// k = 0); R_k += w_n D_k e^{2 pi i k phi_n} (the guess's dedispersed, weighted
-// average, pptoas.py:421-423), each R_k summed by one thread in channel order.
-// Masked channels: sig = dsum = 0 and a zero X row.  No data-spectrum cache
-// (the entry point refuses PPF_SPEC_* for these lengths).  Dynamic LDS: nbin
-// doubles.
-__global__ __launch_bounds__(kBlock) void k_data_xspec_gen(SpecArgs a, int nbin) {
-  extern __shared__ __align__(16) unsigned char gsm[];
-  double* x = reinterpret_cast<double*>(gsm);
-  __shared__ double s_meta[4];
-  __shared__ double red[kWaves];
-  const int c = blockIdx.x, s = a.sub0 + c, tid = threadIdx.x;
-  const int nchan = a.nchan, NH = nbin / 2 + 1;
-  const double* fr = a.freqs + (size_t)s * nchan;
-  const uint8_t* mask = a.mask ? a.mask + (size_t)s * nchan : nullptr;
-  // nu_g (guess dedispersion reference): mean over fitted channels unless given
-  if (tid == 0) {
-    double fs = 0.0, ws = 0.0;
-    int nok = 0;
-    for (int q = 0; q < nchan; ++q) {
-      if (mask && !mask[q]) continue;
-      fs += fr[q];
-      ws += a.weights ? a.weights[(size_t)s * nchan + q] : 1.0;
-      ++nok;
-    }
-    double nug = a.guess_nu ? a.guess_nu[s] : NAN;
-    if (isnan(nug)) nug = fs / nok;
-    s_meta[0] = nug;
-    s_meta[1] = ws;
-    s_meta[2] = (double)nok;
-    s_meta[3] = a.init ? a.init[(size_t)s * 5 + 1] : 0.0;
-  }
-  __syncthreads();
-  const double nug2 = 1.0 / (s_meta[0] * s_meta[0]);
-  const double wsum = s_meta[1];
-  const double Dfac = kDconst * s_meta[3] / a.P[s];
-  const int midx = a.model_idx ? a.model_idx[s] : 0;
-  double2* Rr = a.R + (size_t)c * a.NHP;
-  if (a.guess)
-    for (int k = tid; k < a.NHP; k += kBlock) Rr[k] = cmk(0.0, 0.0);
-  for (int n = 0; n < nchan; ++n) {
-    double2* Xr = a.X + ((size_t)c * nchan + n) * a.NHP;
-    if (mask && !mask[n]) {
-      if (tid == 0) { a.sig[(size_t)c * nchan + n] = 0.0; a.dsum[(size_t)c * nchan + n] = 0.0; }
-      for (int k = tid; k < a.NHP; k += kBlock) Xr[k] = cmk(0.0, 0.0);
-      continue;
-    }
-    __syncthreads();  // the previous row's readers are done with x
-    load_real_row(x, a.data + ((size_t)s * nchan + n) * nbin, nbin);
-    __syncthreads();
-    const double2* Mr = a.M + ((size_t)midx * nchan + n) * a.NHP;
-    const double phi = Dfac * (1.0 / (fr[n] * fr[n]) - nug2);
-    const double wq = a.weights ? a.weights[(size_t)s * nchan + n] : 1.0;
-    double pn = 0.0, pd = 0.0;
-    dft_each_bin(x, nbin, NH, a.tw, [&](int k, double2 d) {
-      const double p2 = cabs2(d);
-      if (k >= a.kc) pn += p2;
-      if (k >= 1) pd += p2;
-      Xr[k] = k >= 1 ? cmulc(d, Mr[k]) : cmk(0.0, 0.0);
-      if (a.guess) Rr[k] = cadd(Rr[k], cmul(d, cscale(turn_phasor((double)k, phi), wq)));
-    });
-    for (int k = NH + tid; k < a.NHP; k += kBlock) Xr[k] = cmk(0.0, 0.0);
-    pn = block_sum(pn, red);
-    pd = block_sum(pd, red);
-    if (tid == 0) {
-      double sig = a.errs ? a.errs[(size_t)s * nchan + n] : NAN;
-      if (isnan(sig)) sig = sqrt(pn / (double)nbin / (double)(NH - a.kc));
-      a.sig[(size_t)c * nchan + n] = sig;
-      a.dsum[(size_t)c * nchan + n] = pd;
-    }
-  }
-  if (a.guess) {
-    const double iw = 1.0 / wsum;
-    for (int k = tid; k < a.NHP; k += kBlock) {
-      double2 r = cmk(0.0, 0.0);
-      if (k < NH) {
-        r = cscale(Rr[k], iw);  // summed by this same thread
-        if (k == 0) r = cmk(0.0, 0.0);
-        if (!(nbin & 1) && k == nbin / 2) r.y = 0.0;  // irfft drops Im(X_N)
-      }
-      Rr[k] = r;
-    }
-  }
 }
 
 // k_rotate_rows for any nbin: rfft, times e^{2 pi i k phase} (rotate_data,
@@ -468,6 +330,195 @@ __global__ __launch_bounds__(kBlock) void k_resid_chi2_gen(ResidArgs a,
   if (threadIdx.x == 0) {
     const double e = a.errs[r];
     a.out[r] = acc / (double)nbin / (e * e) / a.dof;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// The data pass's transforms on the fp64 matrix cores: D = rfft of every row
+// of the chunk as two GEMMs over the pair index m' = 1 .. M = (nbin - 1) / 2,
+//   Re D_k = x_0 + [even] (-1)^k x_{nbin/2} + sum_m' (x_m' + x_{nbin-m'}) cos(2 pi m' k / nbin)
+//   Im D_k =                                sum_m' (x_m' - x_{nbin-m'}) (-sin)(2 pi m' k / nbin)
+// (dft_bin's sums, with every cos / sin an exact table value tw[(m' k) mod
+// nbin] instead of a phasor chain).  Workgroup: 16 rows x 256 bins, wave w
+// the bins k0 + 64 w .. + 63 as four 16 x 16 tiles; per step of 4 pair
+// indices one v_mfma_f64_16x16x4 per tile and part, A = the 16 rows' pair
+// sums (lane l: row l & 15, m' = m0 + (l >> 4)), B = the table values
+// (lane l: m' = m0 + (l >> 4), bin l & 15 of the tile).  Output: D into the
+// X rows (k < nbin/2 + 1); k_data_post_gen turns them into X in place.
+// ---------------------------------------------------------------------------
+typedef double gen_f64x4 __attribute__((ext_vector_type(4)));
+constexpr int kGenLdsTw = 4096;  // 64 KB of LDS
+
+// LTW: the twiddle table staged in LDS (nbin <= kGenLdsTw), else read from L2.
+// The 16 rows' pair sums go through LDS in chunks of kGenChunk pair indices,
+// loaded coalesced (16 threads per row segment) by the whole workgroup.
+constexpr int kGenChunk = 64;
+inline size_t dft_mfma_lds(int nbin, bool ltw) {
+  return (ltw ? (size_t)nbin * sizeof(double2) : 0) + 2 * (size_t)kGenChunk * 16 * sizeof(double);
+}
+template <bool LTW>
+__global__ __launch_bounds__(kBlock) void k_dft_rows_mfma(const double* __restrict__ rows,
+                                                          double2* __restrict__ D, int nrows,
+                                                          int nbin, int NHP,
+                                                          const double2* __restrict__ twg) {
+  extern __shared__ __align__(16) unsigned char gsm[];
+  const double2* tw = twg;
+  double* sp_l = reinterpret_cast<double*>(gsm + (LTW ? (size_t)nbin * sizeof(double2) : 0));
+  double* sm_l = sp_l + kGenChunk * 16;
+  if constexpr (LTW) {
+    double2* t = reinterpret_cast<double2*>(gsm);
+    for (int i = threadIdx.x; i < nbin; i += kBlock) t[i] = twg[i];
+    tw = t;  // published by the chunk loop's first barrier
+  }
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int row0 = blockIdx.x * 16, k0 = blockIdx.y * 256 + w * 64;
+  const int NH = nbin / 2 + 1, M = (nbin - 1) / 2;
+  const bool active = k0 < NH;  // wave-uniform: the wave has bins to compute
+  const int ri = lane & 15, kk = lane >> 4;
+  // the chunk loader: thread t fills pair indices 4 (t & 15) .. + 3 of row t >> 4
+  const int lr = tid >> 4, lq = tid & 15;
+  const bool lrow_ok = row0 + lr < nrows;
+  const double* xl = rows + (size_t)(lrow_ok ? row0 + lr : 0) * nbin;
+  // per tile j: the lane's bin and the table index (m' k) mod nbin at m' = 1 + kk
+  int kj[4], idx[4], stp[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int k = k0 + 16 * j + ri;
+    kj[j] = k < NH ? k : 0;  // bins past the end compute bin 0, never stored
+    idx[j] = (int)(((long long)(1 + kk) * kj[j]) % nbin);
+    stp[j] = (int)((4LL * kj[j]) % nbin);
+  }
+  gen_f64x4 cre[4], cim[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    cre[j] = (gen_f64x4){0.0, 0.0, 0.0, 0.0};
+    cim[j] = cre[j];
+  }
+  for (int c0 = 1; c0 <= M; c0 += kGenChunk) {
+    __syncthreads();  // the previous chunk has been consumed
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int mm = 4 * lq + i, m = c0 + mm;
+      double a = 0.0, b = 0.0;
+      if (lrow_ok && m <= M) {
+        a = xl[m];
+        b = xl[nbin - m];
+      }
+      sp_l[mm * 16 + lr] = a + b;
+      sm_l[mm * 16 + lr] = a - b;
+    }
+    __syncthreads();
+    if (active) {
+      const int nst = min(kGenChunk / 4, (M - c0) / 4 + 1);  // steps with any m' <= M
+      for (int st = 0; st < nst; ++st) {
+        const double sp = sp_l[(4 * st + kk) * 16 + ri], sm = sm_l[(4 * st + kk) * 16 + ri];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const double2 t = tw[idx[j]];
+          cre[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(sp, t.x, cre[j], 0, 0, 0);
+          cim[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(sm, t.y, cim[j], 0, 0, 0);
+          idx[j] += stp[j];
+          if (idx[j] >= nbin) idx[j] -= nbin;
+        }
+      }
+    }
+  }
+  if (!active) return;
+  // lane l holds rows (l >> 4) + 4 r of the tile, bin l & 15 of each tile
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = row0 + kk + 4 * r;
+    if (row >= nrows) continue;
+    const double* xo = rows + (size_t)row * nbin;
+    const double x0 = xo[0], xn = (nbin & 1) ? 0.0 : xo[nbin / 2];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = k0 + 16 * j + ri;
+      if (k < NH) {
+        const double re = cre[j][r] + x0 + ((k & 1) ? -xn : xn);
+        D[(size_t)row * NHP + k] = cmk(re, cim[j][r]);
+      }
+    }
+  }
+}
+
+// The data pass's per-subint part (k_data_xspec's outputs for any nbin) from
+// the spectra k_dft_rows_mfma left in the X rows: sig, dsum, the guess average R (each R_k summed by one thread in
+// channel order) and X = D conj(M) in place (0 at k = 0 and past nbin/2).
+__global__ __launch_bounds__(kBlock) void k_data_post_gen(SpecArgs a, int nbin) {
+  __shared__ double s_meta[4];
+  __shared__ double red[kWaves];
+  const int c = blockIdx.x, s = a.sub0 + c, tid = threadIdx.x;
+  const int nchan = a.nchan, NH = nbin / 2 + 1;
+  const double* fr = a.freqs + (size_t)s * nchan;
+  const uint8_t* mask = a.mask ? a.mask + (size_t)s * nchan : nullptr;
+  if (tid == 0) {
+    double fs = 0.0, ws = 0.0;
+    int nok = 0;
+    for (int q = 0; q < nchan; ++q) {
+      if (mask && !mask[q]) continue;
+      fs += fr[q];
+      ws += a.weights ? a.weights[(size_t)s * nchan + q] : 1.0;
+      ++nok;
+    }
+    double nug = a.guess_nu ? a.guess_nu[s] : NAN;
+    if (isnan(nug)) nug = fs / nok;
+    s_meta[0] = nug;
+    s_meta[1] = ws;
+    s_meta[2] = (double)nok;
+    s_meta[3] = a.init ? a.init[(size_t)s * 5 + 1] : 0.0;
+  }
+  __syncthreads();
+  const double nug2 = 1.0 / (s_meta[0] * s_meta[0]);
+  const double wsum = s_meta[1];
+  const double Dfac = kDconst * s_meta[3] / a.P[s];
+  const int midx = a.model_idx ? a.model_idx[s] : 0;
+  double2* Rr = a.R + (size_t)c * a.NHP;
+  if (a.guess)
+    for (int k = tid; k < a.NHP; k += kBlock) Rr[k] = cmk(0.0, 0.0);
+  for (int n = 0; n < nchan; ++n) {
+    double2* Xr = a.X + ((size_t)c * nchan + n) * a.NHP;
+    if (mask && !mask[n]) {
+      if (tid == 0) { a.sig[(size_t)c * nchan + n] = 0.0; a.dsum[(size_t)c * nchan + n] = 0.0; }
+      for (int k = tid; k < a.NHP; k += kBlock) Xr[k] = cmk(0.0, 0.0);
+      continue;
+    }
+    const double2* Mr = a.M + ((size_t)midx * nchan + n) * a.NHP;
+    const double phi = Dfac * (1.0 / (fr[n] * fr[n]) - nug2);
+    const double wq = a.weights ? a.weights[(size_t)s * nchan + n] : 1.0;
+    double pn = 0.0, pd = 0.0;
+    for (int k = tid; k < a.NHP; k += kBlock) {
+      double2 xk = cmk(0.0, 0.0);
+      if (k < NH) {
+        const double2 d = Xr[k];
+        const double p2 = cabs2(d);
+        if (k >= a.kc) pn += p2;
+        if (k >= 1) pd += p2;
+        if (k >= 1) xk = cmulc(d, Mr[k]);
+        if (a.guess) Rr[k] = cadd(Rr[k], cmul(d, cscale(turn_phasor((double)k, phi), wq)));
+      }
+      Xr[k] = xk;
+    }
+    pn = block_sum(pn, red);
+    pd = block_sum(pd, red);
+    if (tid == 0) {
+      double sig = a.errs ? a.errs[(size_t)s * nchan + n] : NAN;
+      if (isnan(sig)) sig = sqrt(pn / (double)nbin / (double)(NH - a.kc));
+      a.sig[(size_t)c * nchan + n] = sig;
+      a.dsum[(size_t)c * nchan + n] = pd;
+    }
+  }
+  if (a.guess) {
+    const double iw = 1.0 / wsum;
+    for (int k = tid; k < a.NHP; k += kBlock) {
+      double2 r = cmk(0.0, 0.0);
+      if (k < NH) {
+        r = cscale(Rr[k], iw);
+        if (k == 0) r = cmk(0.0, 0.0);
+        if (!(nbin & 1) && k == nbin / 2) r.y = 0.0;
+      }
+      Rr[k] = r;
+    }
   }
 }
 

@@ -766,7 +766,6 @@ __global__ void k_vpow(double2* vp, int nbin, int rows);
 // any nbin (ppfit_generic.hip)
 __global__ void k_model_spec_gen(const double* model, double2* M, double* pn, int NHP, int zero_dc,
                                  const double2* tw, double* M2, int nbin);
-__global__ void k_data_xspec_gen(SpecArgs a, int nbin);
 __global__ void k_rotate_rows_gen(const double* in, const double* phase, const double* tau,
                                   double* out, const double2* tw, int nbin);
 __global__ void k_phase_shift_gen(PhaseShiftArgs a, int nbin);
@@ -777,6 +776,10 @@ __global__ void k_rot_accum_gen(const double* data, const double* phase, const d
                                 double2* partial, int nsub, int nchan, int nsplit,
                                 const double2* tw, int nbin);
 __global__ void k_resid_chi2_gen(ResidArgs a, const double2* tw, int nbin);
+template <bool LTW>
+__global__ void k_dft_rows_mfma(const double* rows, double2* D, int nrows, int nbin, int NHP,
+                                const double2* tw);
+__global__ void k_data_post_gen(SpecArgs a, int nbin);
 __global__ void k_gauss_port(GaussArgs g, const double* freqs, double* out);
 template <typename T>
 __global__ void k_unpack(const T* raw, const double* scl, const double* offs, int nsub, int npol,
