@@ -323,3 +323,35 @@ def test_spline_portrait_resampled_generic(tmp_path, nbin):
     port = np.asarray(port)
     assert port.shape == ref.shape
     assert np.max(np.abs(port - ref)) <= 1e-12 * np.max(np.abs(ref))
+
+
+def test_generic_nbin_pieces_and_chunks_bitwise(eng):
+    """The piece pipeline (two queues, ppf_set_pipeline) and a workspace
+    small enough to split the batch into chunks run the generic data pass on
+    shifted slices: bitwise the single-launch results."""
+    nsub, nchan, nbin = 37, 16, 1000
+    w = synth.make_workload(nsub, nchan, nbin, seed=750)
+    data = synth.workload_data_host(w)
+    nu = O.guess_fit_freq(w.freqs)
+    args = (data, w.model, w.freqs, w.P, [0.0, w.DM0, 0, 0, 0], [1, 1, 0, 0, 0])
+    keys = ["params", "param_errs", "nu_out", "cov", "scales", "red_chi2", "snr", "nfev",
+            "status", "errs"]
+
+    def run():
+        out = eng.fit_batch(*args, nu_fit=[nu] * 3, guess=True)
+        return {k: out[k].cpu().numpy() for k in keys}
+
+    try:
+        eng.set_pipeline(1)
+        ref = run()
+        eng.set_pipeline(3)
+        piped = run()
+        eng.set_pipeline(1)
+        eng.set_workspace_limit(12 * nchan * 1008 * 16 + (1 << 20))  # chunks of ~10 subints
+        chunked = run()
+    finally:
+        eng.set_pipeline(0)
+        eng.set_workspace_limit(32 << 30)
+    for o in (piped, chunked):
+        for k in keys:
+            np.testing.assert_array_equal(o[k], ref[k], err_msg=k)
