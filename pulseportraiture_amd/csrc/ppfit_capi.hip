@@ -144,9 +144,12 @@ int gen_table(ppf_ctx* ctx, std::vector<std::pair<int, double2*>>& cache, int nb
     if (p.first == nbin) { *out = p.second; return PPF_OK; }
   double2* t = nullptr;
   HIPCHK(ctx, hipMalloc(&t, n * sizeof(double2)));
-  cache.push_back({nbin, t});
   make(t);
-  HIPCHK(ctx, hipGetLastError());
+  if (hipGetLastError() != hipSuccess) {  // not cached: the next call builds it again
+    (void)hipFree(t);
+    return fail(ctx, PPF_ERR_DEVICE, "table launch for nbin=%d failed", nbin);
+  }
+  cache.push_back({nbin, t});
   *out = t;
   return PPF_OK;
 }

@@ -37,7 +37,7 @@ def eng():
     return Engine(0)
 
 
-@pytest.mark.parametrize("nbin", [100, 1000, 999, 3000])
+@pytest.mark.parametrize("nbin", [100, 1000, 999, 3000, 8191])
 def test_rotate_rows_generic(eng, nbin):
     rng = np.random.default_rng(nbin)
     rows = rng.standard_normal((5, nbin))
@@ -136,9 +136,10 @@ def _same_status(rc, ref_rc, method):
     return rc == ref_rc
 
 
-@pytest.mark.parametrize("nbin", [1000, 999, 1536, 96])
-def test_fit_generic_nbin_phase_dm(eng, nbin):
-    _vs_oracle(eng, 4, 32, nbin, 700 + nbin, [1, 1, 0, 0, 0])
+@pytest.mark.parametrize("nbin,nchan", [(1000, 32), (999, 32), (1536, 32), (96, 32), (8190, 8),
+                                        (6001, 8)])
+def test_fit_generic_nbin_phase_dm(eng, nbin, nchan):
+    _vs_oracle(eng, 4, nchan, nbin, 700 + nbin, [1, 1, 0, 0, 0])
 
 
 @pytest.mark.parametrize("kw", [dict(exact=True), dict(method="TNC"), dict(method="Newton-CG")])
@@ -201,7 +202,7 @@ def test_get_toas_generic_nbin(tmp_path):
     assert np.all(np.abs(dms - (w.DM0 + w.dDM)) < 6 * np.asarray(gt.DM_errs[0]))
 
 
-@pytest.mark.parametrize("nbin", [1000, 999])
+@pytest.mark.parametrize("nbin", [1000, 999, 8191])
 def test_row_entry_points_generic(eng, nbin):
     """get_noise_PS, irfft, fit_phase_shift (ppalign / pplib FFTFIT), the
     zapping residual chi2 and ppalign's rotate-and-sum at a generic nbin,
