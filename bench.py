@@ -21,10 +21,12 @@ all ranks' TOAs / max-over-ranks time.
 
 Beside value (N = 1, default config): the legs a caller actually gets --
 ``get_toas`` (GetTOAs.get_TOAs end to end on a registered 10k-subint archive,
-TOA records and .tim text included; device-resident and host-resident input)
-and ``ppalign`` (align_archives at config 5, 4096 archives x 256 x 2048,
-niter 3).  Also reported: the roofline of the dominant kernel (HIP-event
-timed on the stream it runs on) and the CPU baseline (the oracle restatement,
+TOA records and .tim text included; device-resident and host-resident input),
+``ppalign`` (align_archives at config 5, 4096 archives x 256 x 2048,
+niter 3) and ``generic_nbin`` (the fit of 2000 subints x 64 channels at
+nbin 2000, not a power of two, beside the same batch at 2048).  Also
+reported: the roofline of the dominant kernel (HIP-event timed on the stream
+it runs on) and the CPU baseline (the oracle restatement,
 one process per available host core) on a bounded sample of the same
 workload, with the oracle/reference time ratio measured in the build
 container per config (tests/golden/timing_r3.json).
@@ -313,6 +315,39 @@ def leg_get_toas(eng, w, data, reps=3, host=False):
     return out, gt
 
 
+def leg_generic_nbin(eng, seed, nsub=2000, nchan=64, nbin=2000, reps=3):
+    """The fit at an nbin that is not a power of two (ppfit_generic.hip: the
+    row rfft as a GEMM on the fp64 matrix cores), beside the same batch at
+    the next power of two.  Synthetic: the template rotated per subint
+    (ppf_rotate_rows) plus Gaussian noise."""
+    import torch
+    from pulseportraiture_amd import synth
+    out = {"nsub": nsub, "nchan": nchan}
+    for nb in (nbin, 1 << (nbin - 1).bit_length()):
+        w = synth.make_workload(1, nchan, nb, seed=seed + nb)
+        g = torch.Generator(device="cuda").manual_seed(seed)
+        ph = torch.rand(nsub, 1, generator=g, device="cuda", dtype=torch.float64) * 0.2 - 0.1
+        model = torch.as_tensor(w.model, device="cuda")
+        data = eng.rotate_rows(model.expand(nsub, nchan, nb).reshape(-1, nb).contiguous(),
+                               ph.expand(nsub, nchan).reshape(-1)).reshape(nsub, nchan, nb)
+        data += 1.5 * torch.randn(data.shape, generator=g, device="cuda", dtype=torch.float64)
+        nu = float(np.mean(w.freqs))
+        args = (data, w.model, w.freqs, w.P, [0.0, w.DM0, 0, 0, 0], [1, 1, 0, 0, 0])
+        eng.fit_batch(*args, nu_fit=[nu] * 3, guess=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            res = eng.fit_batch(*args, nu_fit=[nu] * 3, guess=True)
+        torch.cuda.synchronize()
+        t = (time.perf_counter() - t0) / reps
+        ok = int((res["status"] >= 0).sum().item())
+        key = "nbin_%d" % nb
+        out[key] = {"ms_per_batch": round(t * 1e3, 3), "value": round(nsub / t, 1),
+                    "unit": "TOAs/s", "fits_with_status": ok}
+        del data
+    return out
+
+
 def leg_ppalign(eng, narch, niter, seed):
     """align_archives over narch registered single-subint archives of config
     5's shape (views of one device tensor), niter iterations."""
@@ -556,6 +591,7 @@ def main():
             np.abs(np.asarray(gt.phis[0]) - host["params"][:, 0]) / host["param_errs"][:, 0]))
         legs["get_toas"] = g
         legs["get_toas_host"], _ = leg_get_toas(eng, w, data, reps=1, host=True)
+        legs["generic_nbin"] = leg_generic_nbin(eng, args.seed)
         legs["ppalign"] = leg_ppalign(eng, args.ppalign_narch, args.ppalign_niter, args.seed)
         from pulseportraiture_amd import ppalign as _ppa
         legs["ppalign"]["roofline"] = ppalign_roofline(
