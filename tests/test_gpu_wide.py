@@ -16,8 +16,8 @@ Two kinds of check:
   phase-family Taylor fits with and without pipelined pieces and masked
   channels, GM, the exact sweeps, split scattering fits, TNC, Newton-CG and
   ppalign's data-spectrum cache.
-- nchan = 2112, 4096 and 2100 (the last at nbin 200, with the generic-length
-  data pass, ppfit_generic.hip) against the oracle, at the
+- nchan = 2112, 4096, 2100 (at nbin 200, with the generic-length data pass,
+  ppfit_generic.hip) and PPF_MAX_NCHAN = 16384 against the oracle, at the
   north_star tolerance (|dphi| <= 1e-3 sigma_phi, |dDM| <= 1e-3 sigma_DM)
   with identical solver status.
 - get_TOAs end to end on a 2,304-channel archive whose last 256 channels
@@ -157,7 +157,7 @@ def _vs_oracle(eng, nsub, nchan, nbin, seed, flags=(1, 1, 0, 0, 0), **kw):
     return out
 
 
-@pytest.mark.parametrize("nchan,nbin", [(2112, 256), (4096, 128), (2100, 200)])
+@pytest.mark.parametrize("nchan,nbin", [(2112, 256), (4096, 128), (2100, 200), (16384, 64)])
 def test_wide_nchan_vs_oracle(eng, nchan, nbin):
     _vs_oracle(eng, 3, nchan, nbin, seed=620 + nchan)
 
