@@ -123,16 +123,21 @@ size_t gen_rot_lds(int nbin) {
 
 // the generic-length data pass of n subints: every row's rfft on the matrix
 // cores into the X rows, then the per-subint pass (ppfit_generic.hip)
+// (data-spectrum cache: the spectra into the cache's rows under STORE; under
+// USE they are there already)
 void launch_data_gen(const SpecArgs& sa, int n, int nbin, hipStream_t st) {
   const int nrows = n * sa.nchan, NH = nbin / 2 + 1;
   const double* rows = sa.data + (size_t)sa.sub0 * sa.nchan * nbin;
   const dim3 g((nrows + 15) / 16, (NH + 255) / 256);
-  if (nbin <= kGenLdsTw)
-    hipLaunchKernelGGL(k_dft_rows_mfma<true>, g, dim3(kBlock), dft_mfma_lds(nbin, true), st,
-                       rows, sa.X, nrows, nbin, sa.NHP, sa.tw);
-  else
-    hipLaunchKernelGGL(k_dft_rows_mfma<false>, g, dim3(kBlock), dft_mfma_lds(nbin, false), st,
-                       rows, sa.X, nrows, nbin, sa.NHP, sa.tw);
+  double2* dst = sa.D ? sa.D : sa.X;
+  if (sa.spec_mode != PPF_SPEC_USE) {
+    if (nbin <= kGenLdsTw)
+      hipLaunchKernelGGL(k_dft_rows_mfma<true>, g, dim3(kBlock), dft_mfma_lds(nbin, true), st,
+                         rows, dst, nrows, nbin, sa.NHP, sa.tw);
+    else
+      hipLaunchKernelGGL(k_dft_rows_mfma<false>, g, dim3(kBlock), dft_mfma_lds(nbin, false), st,
+                         rows, dst, nrows, nbin, sa.NHP, sa.tw);
+  }
   hipLaunchKernelGGL(k_data_post_gen, dim3(n), dim3(kBlock), 0, st, sa, nbin);
 }
 
@@ -536,9 +541,6 @@ int ppf_fit_portrait_batch(ppf_ctx* ctx, const ppf_fit_desc* d, const ppf_fit_re
     if (!taylor || d->fit_flags[3] || d->fit_flags[4])
       return fail(ctx, PPF_ERR_UNSUPPORTED, "the data-spectrum cache takes phase-family "
                   "trust-ncg fits only (tau and alpha not fitted, not PPF_SOLVE_EXACT)");
-    if (logN < 0)
-      return fail(ctx, PPF_ERR_UNSUPPORTED, "the data-spectrum cache needs a power-of-two nbin "
-                  "(nbin=%d)", d->nbin);
   }
   // mean template spectrum for the unmasked guess
   double2* Mmean = nullptr;
@@ -1361,7 +1363,7 @@ int ppf_rotate_accumulate(ppf_ctx* ctx, int32_t nsub, int32_t nchan, int32_t nbi
 
 int32_t ppf_spec_nhp(int32_t nbin) {
   int logN;
-  if (check_nbin(nullptr, nbin, &logN)) return -1;
+  if (check_nbin_any(nullptr, nbin, &logN)) return -1;
   return nharm_pad(nbin);
 }
 
@@ -1372,7 +1374,7 @@ int ppf_rotate_accumulate_spec(ppf_ctx* ctx, int32_t nsub, int32_t nchan, int32_
     return fail(ctx, PPF_ERR_INVALID, "null argument");
   if (nsub <= 0 || nchan <= 0) return PPF_OK;
   int logN;
-  if (int r = check_nbin(ctx, nbin, &logN)) return r;
+  if (int r = check_nbin_any(ctx, nbin, &logN)) return r;  // spectra of any length
   HIPCHK(ctx, hipSetDevice(ctx->device));
   const int N = nbin / 2, NH = N + 1, NHP = nharm_pad(nbin);
   // one workgroup per (slice, channel), about 2048 of them (8 per CU)

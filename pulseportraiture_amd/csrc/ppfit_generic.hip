@@ -443,12 +443,21 @@ __global__ __launch_bounds__(kBlock) void k_dft_rows_mfma(const double* __restri
 }
 
 // The data pass's per-subint part (k_data_xspec's outputs for any nbin) from
-// the spectra k_dft_rows_mfma left in the X rows: sig, dsum, the guess average R (each R_k summed by one thread in
-// channel order) and X = D conj(M) in place (0 at k = 0 and past nbin/2).
+// the spectra k_dft_rows_mfma left in the X rows -- or, with the data-spectrum
+// cache (a.D), in the cache's rows: sig, dsum, the guess average R (each R_k
+// summed by one thread in channel order) and X = D conj(M) (0 at k = 0 and
+// past nbin/2), in place or into X.  As k_data_xspec: under PPF_SPEC_STORE /
+// _USE the Taylor-path subints get no X (their moment passes form it from
+// D), under _USE they are not visited at all, and STORE leaves masked rows
+// and the padding of the cached D rows zero.
 __global__ __launch_bounds__(kBlock) void k_data_post_gen(SpecArgs a, int nbin) {
   __shared__ double s_meta[4];
   __shared__ double red[kWaves];
   const int c = blockIdx.x, s = a.sub0 + c, tid = threadIdx.x;
+  const bool tsub = a.D && spec_taylor_sub(a, s);
+  if (a.spec_mode == PPF_SPEC_USE && tsub) return;  // all of it cached
+  const bool wx = !tsub;                                      // X rows wanted
+  const bool wd = a.D != nullptr && a.spec_mode == PPF_SPEC_STORE;  // cache rows to tidy
   const int nchan = a.nchan, NH = nbin / 2 + 1;
   const double* fr = a.freqs + (size_t)s * nchan;
   const uint8_t* mask = a.mask ? a.mask + (size_t)s * nchan : nullptr;
@@ -478,9 +487,13 @@ __global__ __launch_bounds__(kBlock) void k_data_post_gen(SpecArgs a, int nbin) 
     for (int k = tid; k < a.NHP; k += kBlock) Rr[k] = cmk(0.0, 0.0);
   for (int n = 0; n < nchan; ++n) {
     double2* Xr = a.X + ((size_t)c * nchan + n) * a.NHP;
+    double2* Dr = a.D ? a.D + ((size_t)c * nchan + n) * a.NHP : Xr;  // the spectra
     if (mask && !mask[n]) {
       if (tid == 0) { a.sig[(size_t)c * nchan + n] = 0.0; a.dsum[(size_t)c * nchan + n] = 0.0; }
-      for (int k = tid; k < a.NHP; k += kBlock) Xr[k] = cmk(0.0, 0.0);
+      for (int k = tid; k < a.NHP; k += kBlock) {
+        if (wx) Xr[k] = cmk(0.0, 0.0);
+        if (wd) Dr[k] = cmk(0.0, 0.0);
+      }
       continue;
     }
     const double2* Mr = a.M + ((size_t)midx * nchan + n) * a.NHP;
@@ -490,14 +503,16 @@ __global__ __launch_bounds__(kBlock) void k_data_post_gen(SpecArgs a, int nbin) 
     for (int k = tid; k < a.NHP; k += kBlock) {
       double2 xk = cmk(0.0, 0.0);
       if (k < NH) {
-        const double2 d = Xr[k];
+        const double2 d = Dr[k];
         const double p2 = cabs2(d);
         if (k >= a.kc) pn += p2;
         if (k >= 1) pd += p2;
         if (k >= 1) xk = cmulc(d, Mr[k]);
         if (a.guess) Rr[k] = cadd(Rr[k], cmul(d, cscale(turn_phasor((double)k, phi), wq)));
+      } else if (wd) {
+        Dr[k] = cmk(0.0, 0.0);
       }
-      Xr[k] = xk;
+      if (wx) Xr[k] = xk;
     }
     pn = block_sum(pn, red);
     pd = block_sum(pd, red);

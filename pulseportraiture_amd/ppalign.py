@@ -596,9 +596,6 @@ class _UnitStack:
         d = self.pols[0]
         if SPEC_CACHE and isinstance(d, torch.Tensor) and d.device.type == "cuda":
             n, nchan, nbin = d.shape
-            if nbin & (nbin - 1):  # the cache needs a power-of-two nbin (ppfit.h)
-                self._spec = None
-                return None
             from .engine import SpecCache
             need = SpecCache.bytes_for(eng, n, nchan, nbin)
             free, _ = torch.cuda.mem_get_info(d.device)

@@ -158,7 +158,7 @@ def test_fit_generic_nbin_scattering(eng):
 def test_generic_nbin_limits(eng):
     from pulseportraiture_amd.engine import PPFitError
     with pytest.raises(PPFitError, match="nbin"):
-        eng.spec_cache(2, 4, 1000)
+        eng.spec_cache(2, 4, 8200)
     w = synth.make_workload(1, 4, 64, seed=1)
     with pytest.raises(PPFitError, match="nbin"):
         eng.fit_batch(np.zeros((1, 4, 8200)), np.zeros((4, 8200)), w.freqs, w.P, np.zeros(5),
@@ -324,6 +324,32 @@ def test_spline_portrait_resampled_generic(tmp_path, nbin):
     port = np.asarray(port)
     assert port.shape == ref.shape
     assert np.max(np.abs(port - ref)) <= 1e-12 * np.max(np.abs(ref))
+
+
+@pytest.mark.parametrize("nbin", [1000, 999])
+def test_generic_nbin_spec_cache_bitwise(eng, nbin):
+    """ppalign's data-spectrum cache at a generic nbin: the storing fit and
+    the refit from the cache (the data pass skipped) give the fit without a
+    cache, bitwise (the spectra are the same GEMM's, stored or in place)."""
+    nsub, nchan = 9, 24
+    w = synth.make_workload(nsub, nchan, nbin, seed=760 + nbin)
+    data = synth.workload_data_host(w)
+    nu = O.guess_fit_freq(w.freqs)
+    mask = np.ones((nsub, nchan), np.uint8)
+    mask[2, ::5] = 0
+    args = (data, w.model, w.freqs, w.P, [0.0, w.DM0, 0, 0, 0], [1, 1, 0, 0, 0])
+    keys = ["params", "param_errs", "nu_out", "cov", "scales", "red_chi2", "snr", "nfev",
+            "status", "errs", "init_used"]
+
+    def run(**kw):
+        out = eng.fit_batch(*args, nu_fit=[nu] * 3, guess=True, chan_mask=mask, **kw)
+        return {k: out[k].cpu().numpy() for k in keys}
+
+    ref = run()
+    cache = eng.spec_cache(nsub, nchan, nbin)
+    for o in (run(spec_cache=cache), run(spec_cache=cache)):
+        for k in keys:
+            np.testing.assert_array_equal(o[k], ref[k], err_msg=k)
 
 
 def test_generic_nbin_pieces_and_chunks_bitwise(eng):
