@@ -54,9 +54,9 @@
  *    ppf_instrumental_response_rows, ppf_phase_shift_batch,
  *    ppf_rotate_accumulate, ppf_irfft_rows, ppf_noise_rows and
  *    ppf_resid_chi2_rows run direct-sum kernels instead (O(nbin^2) per row;
- *    tests/test_gpu_generic_nbin.py), and so does the data-spectrum cache
- *    (PPF_SPEC_*, ppf_spec_nhp, ppf_rotate_accumulate_spec).  Only
- *    ppf_synth_portraits (the bench's generator) takes powers of two only.
+ *    tests/test_gpu_generic_nbin.py), and so do the data-spectrum cache
+ *    (PPF_SPEC_*, ppf_spec_nhp, ppf_rotate_accumulate_spec) and
+ *    ppf_synth_portraits: every entry point takes any nbin in [64, 8192].
  *  - Channel counts: up to PPF_LDS_NCHAN a fit workgroup keeps its subint's
  *    per-channel tables (frequencies, weights, dispersion derivatives, the
  *    fitted-channel list) in LDS; above it (or under PPF_OPT_HBM_TABLES) the

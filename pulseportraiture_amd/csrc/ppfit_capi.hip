@@ -1300,7 +1300,7 @@ int ppf_synth_portraits(ppf_ctx* ctx, int32_t nsub, int32_t nchan, int32_t nbin,
   if (!ctx || !model || !phase || !data) return fail(ctx, PPF_ERR_INVALID, "null argument");
   if (nsub <= 0 || nchan <= 0) return PPF_OK;
   int logN;
-  if (int r = check_nbin(ctx, nbin, &logN)) return r;
+  if (int r = check_nbin_any(ctx, nbin, &logN)) return r;
   HIPCHK(ctx, hipSetDevice(ctx->device));
   double2* M;
   double* pn;
@@ -1311,6 +1311,10 @@ int ppf_synth_portraits(ppf_ctx* ctx, int32_t nsub, int32_t nchan, int32_t nbin,
   const int64_t rows = (int64_t)nsub * nchan;
   if (rows > 0x7fffffff) return fail(ctx, PPF_ERR_INVALID, "too many rows");
   return timed(ctx, PPF_K_SYNTH, [&] {
+    if (logN < 0)
+      hipLaunchKernelGGL(k_synth_gen, dim3((unsigned)rows), dim3(kBlock),
+                         (size_t)(nbin / 2 + 1) * sizeof(double2), ctx->stream, M, phase, data,
+                         nchan, NHP, sigma, seed, sub0, tw, nbin);
     LOGN_SWITCH(logN, hipLaunchKernelGGL(k_synth<LG>, dim3((unsigned)rows), dim3(kBlock), 0,
                                          ctx->stream, M, phase, data, nchan, NHP, sigma, seed,
                                          sub0, tw));

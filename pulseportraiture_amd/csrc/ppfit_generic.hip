@@ -537,4 +537,40 @@ __global__ __launch_bounds__(kBlock) void k_data_post_gen(SpecArgs a, int nbin) 
   }
 }
 
+// k_synth for any nbin: data[s][n] = irfft(Mfull_n e^{2 pi i k phase[s][n]},
+// n = nbin) + sigma * the Philox normals of k_synth (pair j of samples 2j,
+// 2j + 1 from counter (j, n, s); at odd nbin the last sample takes the first
+// normal of its pair -- synth.noise_block's layout).  Dynamic LDS: nbin/2 + 1
+// double2.
+__global__ __launch_bounds__(kBlock) void k_synth_gen(const double2* __restrict__ Mfull,
+                                                      const double* __restrict__ phase,
+                                                      double* __restrict__ data, int nchan,
+                                                      int NHP, double sigma, uint64_t seed,
+                                                      int64_t sub0,
+                                                      const double2* __restrict__ tw, int nbin) {
+  extern __shared__ __align__(16) unsigned char gsm[];
+  double2* X = reinterpret_cast<double2*>(gsm);
+  const int row = blockIdx.x, n = row % nchan, NH = nbin / 2 + 1;
+  const int64_t s = row / nchan;
+  const double ph = phase[row];
+  for (int k = threadIdx.x; k < NH; k += kBlock)
+    X[k] = cmul(Mfull[(size_t)n * NHP + k], turn_phasor((double)k, ph));
+  __syncthreads();
+  double* out = data + (size_t)row * nbin;
+  idft_row(X, nbin, tw, out);
+  if (sigma == 0.0) return;
+  __syncthreads();  // the block's samples are stored (each pair is then one thread's)
+  const uint64_t gs = (uint64_t)(s + sub0);
+  for (int j = threadIdx.x; 2 * j < nbin; j += kBlock) {
+    u32x4 ctr;
+    ctr.v[0] = (uint32_t)j;
+    ctr.v[1] = (uint32_t)n;
+    ctr.v[2] = (uint32_t)gs;
+    ctr.v[3] = (uint32_t)(gs >> 32);
+    const double2 z = philox_normal2(ctr, seed);
+    out[2 * j] = fma(sigma, z.x, out[2 * j]);
+    if (2 * j + 1 < nbin) out[2 * j + 1] = fma(sigma, z.y, out[2 * j + 1]);
+  }
+}
+
 }  // namespace ppf

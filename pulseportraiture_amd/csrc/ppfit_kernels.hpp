@@ -780,6 +780,9 @@ template <bool LTW>
 __global__ void k_dft_rows_mfma(const double* rows, double2* D, int nrows, int nbin, int NHP,
                                 const double2* tw);
 __global__ void k_data_post_gen(SpecArgs a, int nbin);
+__global__ void k_synth_gen(const double2* Mfull, const double* phase, double* data, int nchan,
+                            int NHP, double sigma, uint64_t seed, int64_t sub0,
+                            const double2* tw, int nbin);
 __global__ void k_gauss_port(GaussArgs g, const double* freqs, double* out);
 template <typename T>
 __global__ void k_unpack(const T* raw, const double* scl, const double* offs, int nsub, int npol,

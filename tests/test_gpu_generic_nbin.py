@@ -382,3 +382,15 @@ def test_generic_nbin_pieces_and_chunks_bitwise(eng):
     for o in (piped, chunked):
         for k in keys:
             np.testing.assert_array_equal(o[k], ref[k], err_msg=k)
+
+
+@pytest.mark.parametrize("nbin", [1000, 999])
+def test_synth_generic(eng, nbin):
+    """The synthetic-portrait generator (k_synth's Philox noise layout) at a
+    generic nbin against its numpy twin, synth.synth_portraits_host."""
+    nchan, nsub = 8, 3
+    model = np.random.default_rng(3).normal(0, 1, (nchan, nbin))
+    ph = np.random.default_rng(4).uniform(-2, 2, (nsub, nchan))
+    got = eng.synth(model, ph, 1.5, 12345, sub0=7).cpu().numpy()
+    ref = synth.synth_portraits_host(model, ph, 1.5, 12345, sub0=7)
+    np.testing.assert_allclose(got, ref, atol=1e-11)
