@@ -97,16 +97,8 @@ int ilog2_exact(int v) {
   return l;
 }
 
-int check_nbin(ppf_ctx* ctx, int nbin, int* logN) {
-  const int l = ilog2_exact(nbin);
-  if (l < 6 || l > 13)
-    return fail(ctx, PPF_ERR_UNSUPPORTED, "nbin=%d: must be a power of two in [64, 8192]", nbin);
-  *logN = l - 1;  // complex FFT length N = nbin / 2
-  return PPF_OK;
-}
-
-// Entry points with a generic-length path (ppfit_generic.hip): any nbin in
-// [64, 8192]; *logN = -1 when nbin is not a power of two.
+// Any nbin in [64, 8192]: *logN = log2(nbin / 2) selects the FFT kernels of
+// a power of two, -1 the generic-length ones (ppfit_generic.hip).
 int check_nbin_any(ppf_ctx* ctx, int nbin, int* logN) {
   if (nbin < 64 || nbin > 8192)
     return fail(ctx, PPF_ERR_UNSUPPORTED, "nbin=%d: outside [64, 8192]", nbin);
