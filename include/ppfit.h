@@ -45,7 +45,7 @@
  *    reduction, 3 linalg error), as returned by the reference's
  *    results.status (pptoaslib.py:1018).
  *  - Shapes (PPF_ERR_UNSUPPORTED with a message outside them, never a
- *    silent fallback): nbin in [64, 8192] and nchan <= PPF_MAX_NCHAN (the
+ *    silent fallback): nbin in [16, 8192] and nchan <= PPF_MAX_NCHAN (the
  *    reference takes any; 16384 channels covers every receiver in use).
  *    The FFT kernels are built per power of two; for any other nbin (the
  *    reference's numpy rfft takes any length, pptoaslib.py:976-978)
@@ -56,7 +56,8 @@
  *    ppf_resid_chi2_rows run direct-sum kernels instead (O(nbin^2) per row;
  *    tests/test_gpu_generic_nbin.py), and so do the data-spectrum cache
  *    (PPF_SPEC_*, ppf_spec_nhp, ppf_rotate_accumulate_spec) and
- *    ppf_synth_portraits: every entry point takes any nbin in [64, 8192].
+ *    ppf_synth_portraits: every entry point takes any nbin in [16, 8192]
+ *    (powers of two below 64 take the generic kernels too).
  *  - Channel counts: up to PPF_LDS_NCHAN a fit workgroup keeps its subint's
  *    per-channel tables (frequencies, weights, dispersion derivatives, the
  *    fitted-channel list) in LDS; above it (or under PPF_OPT_HBM_TABLES) the
@@ -331,8 +332,8 @@ int ppf_gaussian_portraits(ppf_ctx* ctx, int32_t nrow, int32_t nbin, int32_t nga
  * mean_prof + sum_e splev(freqs[r], (t, c[e], k), ext=0) eigvec[:, e]
  * (FITPACK splev / fpbspl); neig == 0 tiles mean_prof.  When nbin_in !=
  * nbin the rows are resampled as scipy.signal.resample (rfft branch) and
- * rotated by 0.5 (1/nbin - 1/nbin_in) (rotate_portrait), both then powers
- * of two in [64, 8192].  t HOST [nknot], c HOST [neig][ncoef] (ncoef >=
+ * rotated by 0.5 (1/nbin - 1/nbin_in) (rotate_portrait), both then in
+ * [16, 8192].  t HOST [nknot], c HOST [neig][ncoef] (ncoef >=
  * nknot - k - 1), 1 <= k <= 5, neig <= 64; mean_prof [nbin_in], eigvec
  * [nbin_in][neig], freqs [nrow], out [nrow][nbin] on the device.          */
 int ppf_spline_portraits(ppf_ctx* ctx, int32_t nrow, int32_t nbin_in, int32_t nbin, int32_t neig,

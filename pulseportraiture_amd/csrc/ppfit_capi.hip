@@ -97,13 +97,14 @@ int ilog2_exact(int v) {
   return l;
 }
 
-// Any nbin in [64, 8192]: *logN = log2(nbin / 2) selects the FFT kernels of
-// a power of two, -1 the generic-length ones (ppfit_generic.hip).
+// Any nbin in [16, 8192]: *logN = log2(nbin / 2) selects the FFT kernels of
+// a power of two from 64 up, -1 the generic-length ones (ppfit_generic.hip)
+// for every other length.
 int check_nbin_any(ppf_ctx* ctx, int nbin, int* logN) {
-  if (nbin < 64 || nbin > 8192)
-    return fail(ctx, PPF_ERR_UNSUPPORTED, "nbin=%d: outside [64, 8192]", nbin);
+  if (nbin < 16 || nbin > 8192)
+    return fail(ctx, PPF_ERR_UNSUPPORTED, "nbin=%d: outside [16, 8192]", nbin);
   const int l = ilog2_exact(nbin);
-  *logN = l < 0 ? -1 : l - 1;
+  *logN = l < 6 ? -1 : l - 1;
   return PPF_OK;
 }
 

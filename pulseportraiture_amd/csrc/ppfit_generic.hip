@@ -3,7 +3,7 @@
 // The reference transforms profiles with numpy's rfft / irfft of whatever
 // length the archive has (pptoaslib.py:976-978, pplib.py:2338-2426).  The
 // register and LDS FFTs of ppfit_spectra.hip are built per power of two; for
-// every other nbin in [64, 8192] these kernels take their place in the fit
+// every other nbin in [16, 8192] these kernels take their place in the fit
 // entry point, the template spectra, the row rotations, FFTFIT, the noise
 // rows, irfft, the zapping residuals and ppalign's rotate-and-sum: the same
 // outputs from direct sums, O(nbin^2) per row instead of O(nbin log nbin).

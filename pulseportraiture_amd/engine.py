@@ -985,7 +985,7 @@ class SpecCache:
     def __init__(self, eng, nsub, nchan, nbin):
         nhp = int(eng.lib.ppf_spec_nhp(int(nbin)))
         if nhp <= 0:
-            raise PPFitError("nbin=%d: outside [64, 8192]" % nbin)
+            raise PPFitError("nbin=%d: outside [16, 8192]" % nbin)
         f64 = dict(dtype=torch.float64, device=eng.device)
         self.nsub, self.nchan, self.nbin, self.nhp = int(nsub), int(nchan), int(nbin), nhp
         self.spec = torch.empty((nsub, nchan, nhp, 2), **f64)

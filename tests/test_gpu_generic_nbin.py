@@ -2,7 +2,7 @@
 
 The reference transforms with numpy's rfft / irfft of any length
 (pptoaslib.py:976-978, pplib.py:2338-2426); the library's FFT kernels are
-built per power of two, and for every other nbin in [64, 8192] the fit entry
+built per power of two, and for every other nbin in [16, 8192] the fit entry
 point, the template spectra, the row rotations and the Gaussian templates
 take direct-sum kernels instead.  Checked here against the oracle (numpy):
 - rotated / scattered rows and Gaussian templates to 1e-12 of the row scale;
@@ -37,7 +37,7 @@ def eng():
     return Engine(0)
 
 
-@pytest.mark.parametrize("nbin", [100, 1000, 999, 3000, 8191])
+@pytest.mark.parametrize("nbin", [16, 33, 100, 1000, 999, 3000, 8191])
 def test_rotate_rows_generic(eng, nbin):
     rng = np.random.default_rng(nbin)
     rows = rng.standard_normal((5, nbin))
@@ -137,7 +137,7 @@ def _same_status(rc, ref_rc, method):
 
 
 @pytest.mark.parametrize("nbin,nchan", [(1000, 32), (999, 32), (1536, 32), (96, 32), (8190, 8),
-                                        (6001, 8)])
+                                        (6001, 8), (32, 32), (48, 16)])
 def test_fit_generic_nbin_phase_dm(eng, nbin, nchan):
     _vs_oracle(eng, 4, nchan, nbin, 700 + nbin, [1, 1, 0, 0, 0])
 
