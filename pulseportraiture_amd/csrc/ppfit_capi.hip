@@ -121,7 +121,7 @@ size_t gen_rot_lds(int nbin) {
 void launch_data_gen(const SpecArgs& sa, int n, int nbin, hipStream_t st) {
   const int nrows = n * sa.nchan, NH = nbin / 2 + 1;
   const double* rows = sa.data + (size_t)sa.sub0 * sa.nchan * nbin;
-  const dim3 g((nrows + 15) / 16, (NH + 255) / 256);
+  const dim3 g((nrows + kGenRows - 1) / kGenRows, (NH + 255) / 256);
   double2* dst = sa.D ? sa.D : sa.X;
   if (sa.spec_mode != PPF_SPEC_USE) {
     if (nbin <= kGenLdsTw)

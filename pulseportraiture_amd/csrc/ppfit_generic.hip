@@ -339,8 +339,8 @@ __global__ __launch_bounds__(kBlock) void k_resid_chi2_gen(ResidArgs a,
 //   Re D_k = x_0 + [even] (-1)^k x_{nbin/2} + sum_m' (x_m' + x_{nbin-m'}) cos(2 pi m' k / nbin)
 //   Im D_k =                                sum_m' (x_m' - x_{nbin-m'}) (-sin)(2 pi m' k / nbin)
 // (dft_bin's sums, with every cos / sin an exact table value tw[(m' k) mod
-// nbin] instead of a phasor chain).  Workgroup: 16 rows x 256 bins, wave w
-// the bins k0 + 64 w .. + 63 as four 16 x 16 tiles; per step of 4 pair
+// nbin] instead of a phasor chain).  Workgroup: 16 kGenRT rows x 256 bins,
+// wave w the bins k0 + 64 w .. + 63 as four 16 x 16 tiles per row tile; per step of 4 pair
 // indices one v_mfma_f64_16x16x4 per tile and part, A = the 16 rows' pair
 // sums (lane l: row l & 15, m' = m0 + (l >> 4)), B = the table values
 // (lane l: m' = m0 + (l >> 4), bin l & 15 of the tile).  Output: D into the
@@ -350,11 +350,19 @@ typedef double gen_f64x4 __attribute__((ext_vector_type(4)));
 constexpr int kGenLdsTw = 4096;  // 64 KB of LDS
 
 // LTW: the twiddle table staged in LDS (nbin <= kGenLdsTw), else read from L2.
-// The 16 rows' pair sums go through LDS in chunks of kGenChunk pair indices,
-// loaded coalesced (16 threads per row segment) by the whole workgroup.
+// Each workgroup takes kGenRT tiles of 16 rows, so every table value a lane
+// gathers feeds kGenRT MFMAs per part; the rows' pair sums go through LDS in
+// chunks of kGenChunk pair indices, loaded coalesced (16 threads per row
+// segment) by the whole workgroup.
+#ifndef PPF_DFT_RT
+#define PPF_DFT_RT 2  // A/B knob: row tiles per workgroup
+#endif
 constexpr int kGenChunk = 64;
+constexpr int kGenRT = PPF_DFT_RT;
+constexpr int kGenRows = 16 * kGenRT;
 inline size_t dft_mfma_lds(int nbin, bool ltw) {
-  return (ltw ? (size_t)nbin * sizeof(double2) : 0) + 2 * (size_t)kGenChunk * 16 * sizeof(double);
+  return (ltw ? (size_t)nbin * sizeof(double2) : 0) +
+         2 * (size_t)kGenChunk * kGenRows * sizeof(double);
 }
 template <bool LTW>
 __global__ __launch_bounds__(kBlock) void k_dft_rows_mfma(const double* __restrict__ rows,
@@ -364,21 +372,20 @@ __global__ __launch_bounds__(kBlock) void k_dft_rows_mfma(const double* __restri
   extern __shared__ __align__(16) unsigned char gsm[];
   const double2* tw = twg;
   double* sp_l = reinterpret_cast<double*>(gsm + (LTW ? (size_t)nbin * sizeof(double2) : 0));
-  double* sm_l = sp_l + kGenChunk * 16;
+  double* sm_l = sp_l + kGenChunk * kGenRows;
   if constexpr (LTW) {
     double2* t = reinterpret_cast<double2*>(gsm);
     for (int i = threadIdx.x; i < nbin; i += kBlock) t[i] = twg[i];
     tw = t;  // published by the chunk loop's first barrier
   }
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int row0 = blockIdx.x * 16, k0 = blockIdx.y * 256 + w * 64;
+  const int row0 = blockIdx.x * kGenRows, k0 = blockIdx.y * 256 + w * 64;
   const int NH = nbin / 2 + 1, M = (nbin - 1) / 2;
   const bool active = k0 < NH;  // wave-uniform: the wave has bins to compute
   const int ri = lane & 15, kk = lane >> 4;
-  // the chunk loader: thread t fills pair indices 4 (t & 15) .. + 3 of row t >> 4
+  // the chunk loader: thread t fills pair indices 4 (t & 15) .. + 3 of rows
+  // (t >> 4) + 16 q, q < kGenRT
   const int lr = tid >> 4, lq = tid & 15;
-  const bool lrow_ok = row0 + lr < nrows;
-  const double* xl = rows + (size_t)(lrow_ok ? row0 + lr : 0) * nbin;
   // per tile j: the lane's bin and the table index (m' k) mod nbin at m' = 1 + kk
   int kj[4], idx[4], stp[4];
 #pragma unroll
@@ -388,35 +395,51 @@ __global__ __launch_bounds__(kBlock) void k_dft_rows_mfma(const double* __restri
     idx[j] = (int)(((long long)(1 + kk) * kj[j]) % nbin);
     stp[j] = (int)((4LL * kj[j]) % nbin);
   }
-  gen_f64x4 cre[4], cim[4];
+  gen_f64x4 cre[kGenRT][4], cim[kGenRT][4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    cre[j] = (gen_f64x4){0.0, 0.0, 0.0, 0.0};
-    cim[j] = cre[j];
-  }
+  for (int q = 0; q < kGenRT; ++q)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      cre[q][j] = (gen_f64x4){0.0, 0.0, 0.0, 0.0};
+      cim[q][j] = cre[q][j];
+    }
   for (int c0 = 1; c0 <= M; c0 += kGenChunk) {
     __syncthreads();  // the previous chunk has been consumed
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int mm = 4 * lq + i, m = c0 + mm;
-      double a = 0.0, b = 0.0;
-      if (lrow_ok && m <= M) {
-        a = xl[m];
-        b = xl[nbin - m];
+    for (int q = 0; q < kGenRT; ++q) {
+      const int lrow = lr + 16 * q;
+      const bool ok = row0 + lrow < nrows;
+      const double* xl = rows + (size_t)(ok ? row0 + lrow : 0) * nbin;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int mm = 4 * lq + i, m = c0 + mm;
+        double a = 0.0, b = 0.0;
+        if (ok && m <= M) {
+          a = xl[m];
+          b = xl[nbin - m];
+        }
+        sp_l[mm * kGenRows + lrow] = a + b;
+        sm_l[mm * kGenRows + lrow] = a - b;
       }
-      sp_l[mm * 16 + lr] = a + b;
-      sm_l[mm * 16 + lr] = a - b;
     }
     __syncthreads();
     if (active) {
       const int nst = min(kGenChunk / 4, (M - c0) / 4 + 1);  // steps with any m' <= M
       for (int st = 0; st < nst; ++st) {
-        const double sp = sp_l[(4 * st + kk) * 16 + ri], sm = sm_l[(4 * st + kk) * 16 + ri];
+        double sp[kGenRT], sm[kGenRT];
+#pragma unroll
+        for (int q = 0; q < kGenRT; ++q) {
+          sp[q] = sp_l[(4 * st + kk) * kGenRows + 16 * q + ri];
+          sm[q] = sm_l[(4 * st + kk) * kGenRows + 16 * q + ri];
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const double2 t = tw[idx[j]];
-          cre[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(sp, t.x, cre[j], 0, 0, 0);
-          cim[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(sm, t.y, cim[j], 0, 0, 0);
+#pragma unroll
+          for (int q = 0; q < kGenRT; ++q) {
+            cre[q][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(sp[q], t.x, cre[q][j], 0, 0, 0);
+            cim[q][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(sm[q], t.y, cim[q][j], 0, 0, 0);
+          }
           idx[j] += stp[j];
           if (idx[j] >= nbin) idx[j] -= nbin;
         }
@@ -424,22 +447,24 @@ __global__ __launch_bounds__(kBlock) void k_dft_rows_mfma(const double* __restri
     }
   }
   if (!active) return;
-  // lane l holds rows (l >> 4) + 4 r of the tile, bin l & 15 of each tile
+  // lane l holds rows (l >> 4) + 4 r of each row tile, bin l & 15 of each bin tile
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int row = row0 + kk + 4 * r;
-    if (row >= nrows) continue;
-    const double* xo = rows + (size_t)row * nbin;
-    const double x0 = xo[0], xn = (nbin & 1) ? 0.0 : xo[nbin / 2];
+  for (int q = 0; q < kGenRT; ++q)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int k = k0 + 16 * j + ri;
-      if (k < NH) {
-        const double re = cre[j][r] + x0 + ((k & 1) ? -xn : xn);
-        D[(size_t)row * NHP + k] = cmk(re, cim[j][r]);
+    for (int r = 0; r < 4; ++r) {
+      const int row = row0 + 16 * q + kk + 4 * r;
+      if (row >= nrows) continue;
+      const double* xo = rows + (size_t)row * nbin;
+      const double x0 = xo[0], xn = (nbin & 1) ? 0.0 : xo[nbin / 2];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = k0 + 16 * j + ri;
+        if (k < NH) {
+          const double re = cre[q][j][r] + x0 + ((k & 1) ? -xn : xn);
+          D[(size_t)row * NHP + k] = cmk(re, cim[q][j][r]);
+        }
       }
     }
-  }
 }
 
 // The data pass's per-subint part (k_data_xspec's outputs for any nbin) from
