@@ -28,6 +28,19 @@ def test_library_exports_all_header_symbols():
     assert lib.ppf_version() == 1
 
 
+def test_spec_nhp_any_nbin():
+    """ppf_spec_nhp (no device needed): the padded harmonic count for every
+    nbin the library takes, [16, 8192] -- powers of two or not -- and -1
+    outside it (include/ppfit.h)."""
+    from pulseportraiture_amd import build, _lib
+    build.build()
+    lib = _lib.load_library()
+    for nbin in (16, 17, 32, 63, 64, 96, 999, 1000, 1536, 2048, 6001, 8191, 8192):
+        assert lib.ppf_spec_nhp(nbin) == ((nbin // 2 + 1) + 15) // 16 * 16, nbin
+    for nbin in (0, 8, 15, 8193, 16384, -4):
+        assert lib.ppf_spec_nhp(nbin) == -1, nbin
+
+
 def test_binding_covers_header():
     from pulseportraiture_amd import _lib
     assert set(header_symbols()) == set(_lib.EXPORTS)
