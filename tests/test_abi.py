@@ -41,6 +41,17 @@ def test_spec_nhp_any_nbin():
         assert lib.ppf_spec_nhp(nbin) == -1, nbin
 
 
+def test_binding_options_match_header():
+    """_lib.OPTIONS carries every PPF_OPT_* of include/ppfit.h with its id."""
+    from pulseportraiture_amd import _lib
+    txt = open(os.path.join(ROOT, "include", "ppfit.h")).read()
+    opts = {m.group(1).lower(): int(m.group(2))
+            for m in re.finditer(r"#define PPF_OPT_([A-Z_]+) (\d+)", txt)}
+    assert opts == _lib.OPTIONS
+    n = int(re.search(r"#define PPF_NUM_OPTS (\d+)", txt).group(1))
+    assert sorted(opts.values()) == list(range(n))
+
+
 def test_binding_covers_header():
     from pulseportraiture_amd import _lib
     assert set(header_symbols()) == set(_lib.EXPORTS)
